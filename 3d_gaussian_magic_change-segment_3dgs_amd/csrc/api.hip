@@ -1,0 +1,240 @@
+// api.hip -- the C ABI of include/gsr.h: buffer carving and stage orchestration.
+// Reference orchestration: DGR/cuda_rasterizer/rasterizer_impl.cu:198-458 and
+// the host bindings DGR/rasterize_points.cu:35-242.
+#include <stdio.h>
+#include <string>
+
+#include "gsr_internal.h"
+
+namespace {
+thread_local std::string g_last_error;
+
+int fail(const std::string& msg) {
+    g_last_error = msg;
+    return 1;
+}
+
+// Launch errors are checked after every stage; in debug mode the stream is also
+// synchronised so that asynchronous faults are attributed to their stage
+// (reference CHECK_CUDA, auxiliary.h:166-173).
+int check(const char* stage, hipStream_t st, bool debug) {
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && debug) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(std::string("[gsr] ") + stage + ": " + hipGetErrorString(e));
+    return 0;
+}
+
+#define GSR_STAGE(name)                              \
+    do {                                             \
+        if (int rc_ = check(name, st, dbg)) return rc_; \
+    } while (0)
+
+template <typename T>
+T* at(char* base, size_t off) {
+    return reinterpret_cast<T*>(base + off);
+}
+
+int validate(const gsr_settings* s, const gsr_inputs* in, bool forward) {
+    if (!s || !in) return fail("[gsr] null settings/inputs");
+    if (s->P < 0 || s->W <= 0 || s->H <= 0) return fail("[gsr] invalid problem size");
+    if (s->P == 0) return 0;
+    if (!in->means3D || (forward && !in->opacities)) return fail("[gsr] means3D and opacities are required");
+    if ((in->shs == nullptr) == (in->colors_precomp == nullptr))
+        return fail("[gsr] Please provide excatly one of either SHs or precomputed colors!");
+    const bool have_sr = in->scales && in->rotations;
+    if (have_sr == (in->cov3D_precomp != nullptr) || ((in->scales == nullptr) != (in->rotations == nullptr)))
+        return fail("[gsr] Please provide exactly one of either scale/rotation pair or precomputed 3D covariance!");
+    if (in->shs && (s->D < 0 || s->D > 3 || s->M < (s->D + 1) * (s->D + 1)))
+        return fail("[gsr] SH degree must be 0..3 with shs.shape[1] >= (degree+1)^2");
+    if (!s->bg || !s->viewmatrix || !s->projmatrix || !s->campos) return fail("[gsr] missing camera tensors");
+    if (((uintptr_t)in->rotations & 15) || ((uintptr_t)in->segments & 7))
+        return fail("[gsr] rotations must be 16-byte and segments 8-byte aligned");
+    if ((size_t)((s->W + gsr::BX - 1) / gsr::BX) > 65535 || (size_t)((s->H + gsr::BY - 1) / gsr::BY) > 65535)
+        return fail("[gsr] image too large");
+    return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+const char* gsr_last_error(void) { return g_last_error.c_str(); }
+
+const char* gsr_version(void) { return "gsr 0.1 (gfx950)"; }
+
+size_t gsr_geom_bytes(int P) { return gsr::geom_layout(P > 0 ? (size_t)P : 0).bytes; }
+size_t gsr_binning_bytes(int num_rendered) { return gsr::bin_layout(num_rendered > 0 ? (size_t)num_rendered : 0).bytes; }
+size_t gsr_img_bytes(int W, int H) { return gsr::img_layout(W, H).bytes; }
+size_t gsr_backward_scratch_bytes(int num_rendered) {
+    return (num_rendered > 0 ? (size_t)num_rendered : 0) * 12 * sizeof(float) + gsr::ALIGN;
+}
+
+int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* stream,
+                         int* num_rendered) {
+    using namespace gsr;
+    g_last_error.clear();
+    if (int rc = validate(s, in, true)) return rc;
+    if (!num_rendered) return fail("[gsr] num_rendered is NULL");
+    *num_rendered = 0;
+    const int P = s->P;
+    if (P == 0) return 0;
+    if (!geom || !radii) return fail("[gsr] geom/radii buffers are NULL");
+    hipStream_t st = (hipStream_t)stream;
+    const bool dbg = s->debug != 0;
+    const ImgLayout IL = img_layout(s->W, s->H);
+    const GeomLayout L = geom_layout(P);
+    char* g = aligned_base(geom);
+    launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
+                      at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect), st);
+    GSR_STAGE("preprocess");
+    // Depth order: 32-bit keys -> 4 passes (even: sorted keys land back in depth_keys).
+    launch_radix_sort(at<uint32_t>(g, L.depth_keys), nullptr, at<uint32_t>(g, L.dkeys_alt),
+                      at<uint32_t>(g, L.order_alt), at<uint32_t>(g, L.depth_keys), at<uint32_t>(g, L.order), P, 32,
+                      at<uint32_t>(g, L.hist), at<uint32_t>(g, L.parts), st);
+    GSR_STAGE("depth sort");
+    launch_scan_inclusive_gather(at<uint32_t>(g, L.tiles_touched), at<uint32_t>(g, L.order),
+                                 at<uint32_t>(g, L.offsets), P, at<uint32_t>(g, L.parts), st);
+    GSR_STAGE("scan");
+    uint32_t total = 0;
+    hipError_t e = hipMemcpyAsync(&total, at<uint32_t>(g, L.offsets) + (P - 1), sizeof(uint32_t),
+                                  hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(std::string("[gsr] num_rendered copy: ") + hipGetErrorString(e));
+    if (total > 0x7FFFFFFFu) return fail("[gsr] num_rendered overflows int32");
+    *num_rendered = (int)total;
+    return 0;
+}
+
+int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, void* binning, void* img,
+                       int num_rendered, float* out_color, float* out_depth, float* out_alpha, float* out_segment,
+                       void* stream) {
+    using namespace gsr;
+    g_last_error.clear();
+    if (int rc = validate(s, in, true)) return rc;
+    if (!img || !out_color || !out_depth || !out_alpha || !out_segment) return fail("[gsr] null output buffer");
+    hipStream_t st = (hipStream_t)stream;
+    const bool dbg = s->debug != 0;
+    const int P = s->P;
+    const size_t I = num_rendered > 0 ? (size_t)num_rendered : 0;
+    const ImgLayout IL = img_layout(s->W, s->H);
+    const int T = IL.gx * IL.gy;
+    char* im = aligned_base(img);
+    uint2* ranges = at<uint2>(im, IL.ranges);
+    if (hipMemsetAsync(ranges, 0, (size_t)T * sizeof(uint2), st) != hipSuccess) return fail("[gsr] memset ranges");
+    const GeomLayout GL = geom_layout(P > 0 ? P : 0);
+    char* g = P > 0 ? aligned_base(geom) : nullptr;
+    const BinLayout BL = bin_layout(I);
+    char* b = I > 0 ? aligned_base(binning) : nullptr;
+    uint32_t* point_list = nullptr;
+    if (I > 0) {
+        if (!geom || !binning) return fail("[gsr] geom/binning buffers are NULL");
+        launch_duplicate(P, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets), at<uint32_t>(g, GL.tiles_touched),
+                         at<ushort4>(g, GL.rect), IL.gx, at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid),
+                         at<uint32_t>(g, GL.goff), st);
+        GSR_STAGE("duplicate");
+        const int bits = (int)higher_msb((uint32_t)T);
+        const int passes = (bits + RADIX_BITS - 1) / RADIX_BITS;
+        // even pass count: sorted keys return to tkeys; odd: they land in tkeys_alt.
+        uint32_t* kin = at<uint32_t>(b, BL.tkeys);
+        uint32_t* kalt = at<uint32_t>(b, BL.tkeys_alt);
+        uint32_t* kout = (passes % 2 == 0) ? kin : kalt;
+        uint32_t* ktmp = (passes % 2 == 0) ? kalt : kin;
+        launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout, at<uint32_t>(b, BL.slot_vals), I,
+                          bits, at<uint32_t>(b, BL.hist), at<uint32_t>(b, BL.parts), st);
+        GSR_STAGE("tile sort");
+        point_list = at<uint32_t>(b, BL.point_list);
+        launch_finalize(I, kout, at<uint32_t>(b, BL.slot_vals), at<uint32_t>(b, BL.slot_gid), point_list, ranges, st);
+        GSR_STAGE("tile ranges");
+    }
+    launch_render_forward(s->W, s->H, IL.gx, IL.gy, ranges, point_list, g ? at<float4>(g, GL.rec) : nullptr, s->bg,
+                          out_color, out_depth, out_alpha, out_segment, at<uint32_t>(im, IL.n_contrib), st);
+    GSR_STAGE("render");
+    return 0;
+}
+
+int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, void* geom, void* binning,
+                 void* img, int num_rendered, const float* alpha, const float* dL_dcolor, const float* dL_dsegment,
+                 const float* dL_ddepth, const float* dL_dalpha, void* scratch, const gsr_grads* grads,
+                 void* stream) {
+    using namespace gsr;
+    g_last_error.clear();
+    if (int rc = validate(s, in, false)) return rc;
+    if (!grads) return fail("[gsr] grads is NULL");
+    const int P = s->P;
+    if (P == 0) return 0;
+    if (!geom || !img || !radii || !alpha || !dL_dcolor || !dL_dsegment || !dL_ddepth || !dL_dalpha)
+        return fail("[gsr] null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    const bool dbg = s->debug != 0;
+    const size_t I = num_rendered > 0 ? (size_t)num_rendered : 0;
+    const ImgLayout IL = img_layout(s->W, s->H);
+    char* im = aligned_base(img);
+    const GeomLayout GL = geom_layout(P);
+    char* g = aligned_base(geom);
+    float* contrib = nullptr;
+    if (I > 0) {
+        if (!binning || !scratch) return fail("[gsr] binning/scratch buffer is NULL");
+        const BinLayout BL = bin_layout(I);
+        char* b = aligned_base(binning);
+        contrib = reinterpret_cast<float*>(aligned_base(scratch));
+        launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint2>(im, IL.ranges), at<uint32_t>(b, BL.point_list),
+                               at<uint32_t>(b, BL.slot_vals), at<float4>(g, GL.rec), s->bg, alpha,
+                               at<uint32_t>(im, IL.n_contrib), dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha,
+                               contrib, st);
+        GSR_STAGE("render backward");
+    }
+    launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
+                             at<uint8_t>(g, GL.clamped), contrib, *grads, st);
+    GSR_STAGE("gaussian backward");
+    return 0;
+}
+
+long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered, void* geom, void* binning,
+                         void* img, void* dst, void* stream) {
+    using namespace gsr;
+    g_last_error.clear();
+    if (!name || !dst) {
+        fail("[gsr] debug_copy: null argument");
+        return -1;
+    }
+    const std::string n(name);
+    const size_t Pz = P > 0 ? (size_t)P : 0, I = num_rendered > 0 ? (size_t)num_rendered : 0;
+    const GeomLayout GL = geom_layout(Pz);
+    const BinLayout BL = bin_layout(I);
+    const ImgLayout IL = img_layout(W, H);
+    const size_t T = (size_t)IL.gx * IL.gy;
+    const char* src = nullptr;
+    size_t bytes = 0;
+    auto G = [&](size_t off, size_t b) { if (geom) { src = aligned_base(geom) + off; bytes = b; } };
+    auto B = [&](size_t off, size_t b) { if (binning) { src = aligned_base(binning) + off; bytes = b; } };
+    auto M = [&](size_t off, size_t b) { if (img) { src = aligned_base(img) + off; bytes = b; } };
+    if (n == "tiles_touched") G(GL.tiles_touched, Pz * 4);
+    else if (n == "rec") G(GL.rec, Pz * 64);
+    else if (n == "clamped") G(GL.clamped, Pz);
+    else if (n == "order") G(GL.order, Pz * 4);
+    else if (n == "goff") G(GL.goff, Pz * 4);
+    else if (n == "point_list") B(BL.point_list, I * 4);
+    else if (n == "slot_vals") B(BL.slot_vals, I * 4);
+    else if (n == "ranges") M(IL.ranges, T * 8);
+    else if (n == "n_contrib_tiles") M(IL.n_contrib, T * TILE_PIX * 4);
+    else return -1;
+    if (bytes == 0) return 0;
+    if (!src) return -1;
+    if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess) return -1;
+    return (long long)bytes;
+}
+
+int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream) {
+    (void)projmatrix;  // the reference computes p_proj but only tests view-space z (auxiliary.h:154)
+    g_last_error.clear();
+    if (P < 0) return fail("[gsr] invalid P");
+    if (P == 0) return 0;
+    if (!means3D || !viewmatrix || !present) return fail("[gsr] null buffer");
+    hipStream_t st = (hipStream_t)stream;
+    gsr::launch_mark_visible(P, means3D, viewmatrix, present, st);
+    if (int rc = check("mark_visible", st, false)) return rc;
+    return 0;
+}
+
+}  // extern "C"

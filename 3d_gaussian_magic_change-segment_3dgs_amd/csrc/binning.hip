@@ -1,0 +1,311 @@
+// binning.hip -- prefix scan, stable LSD radix sort, key duplication and tile
+// ranges.  Replaces the reference's CUB DeviceScan / DeviceRadixSort calls and
+// the duplicateWithKeys / identifyTileRanges kernels
+// (DGR/cuda_rasterizer/rasterizer_impl.cu:68-138, :281, :304-322).
+//
+// Ordering contract (bit-exact with the reference): the reference sorts
+// (tile << 32 | depth_bits) with a stable sort whose input is emitted in
+// Gaussian-index order, so inside a tile the order is (depth_bits, gaussian).
+// gsr reaches the same total order in two cheaper steps:
+//   1. stable sort of the P depth keys (value = gaussian id)  -> order[]
+//   2. instances are emitted in that depth order, so the instance slot u is
+//      increasing in (depth, gaussian); a stable sort of the I tile keys with
+//      u as the value then yields (tile, depth, gaussian) -- the reference's
+//      order -- after only ceil(log2(T)/8) passes over I instead of
+//      ceil((32+log2 T)/8) passes over 64-bit keys.
+#include "gsr_internal.h"
+
+namespace gsr {
+
+namespace {
+
+__device__ __forceinline__ uint64_t lanemask_lt() {
+    const uint32_t lane = threadIdx.x & 63;
+    return lane ? (~0ull >> (64 - lane)) : 0ull;
+}
+
+// Exclusive scan of one value per thread over a 256-thread block.
+// wsum: __shared__ uint32_t[4].  Returns the exclusive prefix; *total = block sum.
+__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        uint32_t s = wsum[w];
+        if (w < wid) pre += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + x - v;
+}
+
+// ---------------------------------------------------------------- scan ----
+// value(i) = gather ? src[gather[i]] : src[i]
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(const uint32_t* __restrict__ src,
+                                                              const uint32_t* __restrict__ gather, size_t n,
+                                                              uint32_t* __restrict__ parts) {
+    __shared__ uint32_t wsum[4];
+    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        size_t idx = base + (size_t)i * SCAN_THREADS + threadIdx.x;
+        if (idx < n) acc += gather ? src[gather[idx]] : src[idx];
+    }
+    uint32_t tot;
+    block_exclusive_scan(acc, wsum, &tot);
+    if (threadIdx.x == 0) parts[blockIdx.x] = tot;
+}
+
+// Single block: exclusive scan of parts[0..np) in place.
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_parts(uint32_t* __restrict__ parts, size_t np) {
+    __shared__ uint32_t wsum[4];
+    uint32_t carry = 0;
+    for (size_t base = 0; base < np; base += (size_t)SCAN_THREADS * SCAN_ITEMS) {
+        uint32_t v[SCAN_ITEMS];
+        uint32_t s = 0;
+        const size_t mine = base + (size_t)threadIdx.x * SCAN_ITEMS;
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            v[i] = (mine + i < np) ? parts[mine + i] : 0u;
+            s += v[i];
+        }
+        uint32_t tot;
+        uint32_t pre = block_exclusive_scan(s, wsum, &tot) + carry;
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            if (mine + i < np) parts[mine + i] = pre;
+            pre += v[i];
+        }
+        carry += tot;
+    }
+}
+
+// out[i] = (inclusive ? sum_{j<=i} : sum_{j<i}) value(j); tile staged through LDS so
+// both the loads and the stores are coalesced.
+template <bool INCLUSIVE>
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan_down(const uint32_t* __restrict__ src,
+                                                            const uint32_t* __restrict__ gather, size_t n,
+                                                            const uint32_t* __restrict__ parts,
+                                                            uint32_t* __restrict__ out) {
+    __shared__ uint32_t tile[SCAN_TILE + SCAN_TILE / 32];
+    __shared__ uint32_t wsum[4];
+    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+    auto pad = [](int i) { return i + (i >> 5); };
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        int li = i * SCAN_THREADS + threadIdx.x;
+        size_t idx = base + li;
+        tile[pad(li)] = idx < n ? (gather ? src[gather[idx]] : src[idx]) : 0u;
+    }
+    __syncthreads();
+    uint32_t v[SCAN_ITEMS], s = 0;
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        v[i] = tile[pad(threadIdx.x * SCAN_ITEMS + i)];
+        s += v[i];
+    }
+    uint32_t tot;
+    uint32_t pre = block_exclusive_scan(s, wsum, &tot) + parts[blockIdx.x];
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        uint32_t nx = pre + v[i];
+        tile[pad(threadIdx.x * SCAN_ITEMS + i)] = INCLUSIVE ? nx : pre;
+        pre = nx;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) {
+        int li = i * SCAN_THREADS + threadIdx.x;
+        size_t idx = base + li;
+        if (idx < n) out[idx] = tile[pad(li)];
+    }
+}
+
+// ---------------------------------------------------------- radix sort ----
+// Per-block digit histogram -> hist[digit * nblocks + block].
+__global__ void __launch_bounds__(SORT_THREADS) k_radix_upsweep(const uint32_t* __restrict__ keys, size_t n,
+                                                                int shift, uint32_t mask,
+                                                                uint32_t* __restrict__ hist) {
+    __shared__ uint32_t cnt[RADIX];
+    cnt[threadIdx.x] = 0;
+    __syncthreads();
+    const size_t base = (size_t)blockIdx.x * SORT_TILE;
+#pragma unroll
+    for (int i = 0; i < SORT_ITEMS; ++i) {
+        size_t idx = base + (size_t)i * SORT_THREADS + threadIdx.x;
+        if (idx < n) atomicAdd(&cnt[(keys[idx] >> shift) & mask], 1u);
+    }
+    __syncthreads();
+    hist[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = cnt[threadIdx.x];
+}
+
+// Stable scatter.  Elements are ranked round by round (256 per round, in index
+// order); inside a round, a wave64 multi-split by ballots gives each element its
+// rank among equal digits of its wave, and per-wave digit counts in LDS order the
+// four waves.  vals_in == NULL means value = element index.
+__global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
+    const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
+    uint32_t* __restrict__ vals_out, size_t n, int shift, int bits, const uint32_t* __restrict__ hist) {
+    __shared__ uint32_t base_off[RADIX];
+    __shared__ uint32_t wcnt[4][RADIX];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t mask = (1u << bits) - 1u;
+    base_off[tid] = hist[(size_t)tid * gridDim.x + blockIdx.x];
+    const size_t base = (size_t)blockIdx.x * SORT_TILE;
+    const uint64_t lt = lanemask_lt();
+    for (int r = 0; r < SORT_ITEMS; ++r) {
+#pragma unroll
+        for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
+        const size_t idx = base + (size_t)r * SORT_THREADS + tid;
+        const bool valid = idx < n;
+        uint32_t key = 0, val = 0, digit = 0;
+        if (valid) {
+            key = keys_in[idx];
+            val = vals_in ? vals_in[idx] : (uint32_t)idx;
+            digit = (key >> shift) & mask;
+        }
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < bits; ++b) {
+            const bool set = (digit >> b) & 1u;
+            const uint64_t m = __ballot(set);
+            peers &= set ? m : ~m;
+        }
+        const uint32_t rank = __popcll(peers & lt);
+        const uint32_t wtotal = __popcll(peers);
+        __syncthreads();  // wcnt zeroed
+        if (valid && rank == 0) wcnt[wid][digit] = wtotal;
+        __syncthreads();
+        if (valid) {
+            uint32_t pos = base_off[digit] + rank;
+            for (int w = 0; w < wid; ++w) pos += wcnt[w][digit];
+            keys_out[pos] = key;
+            vals_out[pos] = val;
+        }
+        __syncthreads();
+        base_off[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
+        __syncthreads();
+    }
+}
+
+// ----------------------------------------------------------- duplicate ----
+// One thread per depth-ordered Gaussian: emit its tiles (y outer, x inner, as
+// rasterizer_impl.cu:98-108) into consecutive instance slots.
+__global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __restrict__ order,
+                                                   const uint32_t* __restrict__ offsets,
+                                                   const uint32_t* __restrict__ tiles_touched,
+                                                   const ushort4* __restrict__ rect, int gx,
+                                                   uint32_t* __restrict__ tkeys, uint32_t* __restrict__ slot_gid,
+                                                   uint32_t* __restrict__ goff) {
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= P) return;
+    const uint32_t g = order[r];
+    const uint32_t cnt = tiles_touched[g];
+    if (cnt == 0) return;
+    uint32_t off = r == 0 ? 0u : offsets[r - 1];
+    goff[g] = off;
+    const ushort4 rc = rect[g];
+    for (int y = rc.y; y < rc.w; ++y)
+        for (int x = rc.x; x < rc.z; ++x) {
+            tkeys[off] = (uint32_t)(y * gx + x);
+            slot_gid[off] = g;
+            ++off;
+        }
+}
+
+// point_list[k] = gaussian of sorted instance k; tile ranges [first, last+1).
+__global__ void __launch_bounds__(256) k_finalize(size_t I, const uint32_t* __restrict__ tkeys,
+                                                  const uint32_t* __restrict__ slot_vals,
+                                                  const uint32_t* __restrict__ slot_gid,
+                                                  uint32_t* __restrict__ point_list, uint2* __restrict__ ranges) {
+    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= I) return;
+    point_list[k] = slot_gid[slot_vals[k]];
+    const uint32_t t = tkeys[k];
+    if (k == 0 || tkeys[k - 1] != t) ranges[t].x = (uint32_t)k;
+    if (k == I - 1 || tkeys[k + 1] != t) ranges[t].y = (uint32_t)(k + 1);
+}
+
+}  // namespace
+
+// rasterizer_impl.cu:35-50
+uint32_t higher_msb(uint32_t n) {
+    uint32_t msb = sizeof(n) * 4, step = msb;
+    while (step > 1) {
+        step /= 2;
+        if (n >> msb) msb += step; else msb -= step;
+    }
+    if (n >> msb) msb++;
+    return msb;
+}
+
+static void scan_exclusive_inplace(uint32_t* data, size_t n, uint32_t* parts, hipStream_t st) {
+    const size_t nb = cdiv(n, SCAN_TILE);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_THREADS), 0, st, data, nullptr, n, parts);
+    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(SCAN_THREADS), 0, st, parts, nb);
+    hipLaunchKernelGGL(k_scan_down<false>, dim3(nb), dim3(SCAN_THREADS), 0, st, data, nullptr, n, parts, data);
+}
+
+void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
+                                  uint32_t* parts, hipStream_t st) {
+    if (n == 0) return;
+    const size_t nb = cdiv(n, SCAN_TILE);
+    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_THREADS), 0, st, src, gather_idx, n, parts);
+    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(SCAN_THREADS), 0, st, parts, nb);
+    hipLaunchKernelGGL(k_scan_down<true>, dim3(nb), dim3(SCAN_THREADS), 0, st, src, gather_idx, n, parts, out);
+}
+
+// Stable LSD sort of (keys, vals) on the low key_bits bits.  Ping-pongs between
+// (keys_tmp, vals_tmp) and (keys_out, vals_out); the result always lands in
+// (keys_out, vals_out).  keys_in/vals_in are not modified.
+void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_tmp, uint32_t* vals_tmp,
+                       uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits, uint32_t* hist,
+                       uint32_t* parts, hipStream_t st) {
+    if (n == 0) return;
+    if (key_bits < 1) key_bits = 1;
+    const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
+    const size_t nb = sort_blocks(n);
+    const uint32_t* kin = keys_in;
+    const uint32_t* vin = vals_in;
+    for (int p = 0; p < passes; ++p) {
+        const int shift = p * RADIX_BITS;
+        const int bits = key_bits - shift < RADIX_BITS ? key_bits - shift : RADIX_BITS;
+        // last pass writes the output pair; earlier passes alternate so that holds
+        const bool to_out = ((passes - 1 - p) % 2) == 0;
+        uint32_t* kout = to_out ? keys_out : keys_tmp;
+        uint32_t* vout = to_out ? vals_out : vals_tmp;
+        hipLaunchKernelGGL(k_radix_upsweep, dim3(nb), dim3(SORT_THREADS), 0, st, kin, n, shift,
+                           (1u << bits) - 1u, hist);
+        scan_exclusive_inplace(hist, (size_t)RADIX * nb, parts, st);
+        hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, st, kin, vin, kout, vout, n, shift,
+                           bits, hist);
+        kin = kout;
+        vin = vout;
+    }
+}
+
+void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
+                      const ushort4* rect, int gx, uint32_t* tkeys, uint32_t* slot_gid, uint32_t* goff,
+                      hipStream_t st) {
+    if (P == 0) return;
+    hipLaunchKernelGGL(k_duplicate, dim3(cdiv(P, 256)), dim3(256), 0, st, P, order, offsets, tiles_touched, rect,
+                       gx, tkeys, slot_gid, goff);
+}
+
+void launch_finalize(size_t I, const uint32_t* tkeys, const uint32_t* slot_vals, const uint32_t* slot_gid,
+                     uint32_t* point_list, uint2* ranges, hipStream_t st) {
+    if (I == 0) return;
+    hipLaunchKernelGGL(k_finalize, dim3(cdiv(I, 256)), dim3(256), 0, st, I, tkeys, slot_vals, slot_gid,
+                       point_list, ranges);
+}
+
+}  // namespace gsr

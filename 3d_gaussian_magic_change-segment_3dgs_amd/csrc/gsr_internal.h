@@ -1,0 +1,134 @@
+// gsr_internal.h -- shared layout + launch declarations of libgsr (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stddef.h>
+
+#include "../../include/gsr.h"
+
+namespace gsr {
+
+constexpr int BX = GSR_BLOCK_X, BY = GSR_BLOCK_Y;
+constexpr int NCH = GSR_NUM_CHANNELS, NCLS = GSR_NUM_CLASS;
+constexpr int TILE_PIX = BX * BY;  // 256 pixels per tile, 4 per lane of one wave64
+
+// Per-Gaussian render record (64 B, one HBM sector pair, never crosses a 128 B line):
+//   r0 = {x, y, conic.x, conic.y}   r1 = {conic.z, opacity, depth, seg0}
+//   r2 = {r, g, b, seg1}            r3 = reserved (0)
+constexpr int REC_F4 = 4;
+
+// Radix sort / scan tiling (256-thread blocks = 4 wave64s, 16 items per thread).
+constexpr int SORT_THREADS = 256, SORT_ITEMS = 16, SORT_TILE = SORT_THREADS * SORT_ITEMS;
+constexpr int SCAN_THREADS = 256, SCAN_ITEMS = 16, SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+constexpr int RADIX_BITS = 8, RADIX = 1 << RADIX_BITS;
+
+constexpr size_t ALIGN = 256;
+inline size_t align_up(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
+inline size_t cdiv(size_t a, size_t b) { return (a + b - 1) / b; }
+
+inline size_t sort_blocks(size_t n) { return n ? cdiv(n, SORT_TILE) : 0; }
+inline size_t hist_len(size_t n) { return (size_t)RADIX * sort_blocks(n); }
+inline size_t scan_parts(size_t n) { return cdiv(n > 0 ? n : 1, SCAN_TILE) + 1; }
+
+// ---- geometry buffer (reference GeometryState, rasterizer_impl.cu:155-171) ----
+struct GeomLayout {
+    size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, goff,
+        hist, parts, bytes;
+};
+inline GeomLayout geom_layout(size_t P) {
+    GeomLayout L{};
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes); return r; };
+    L.rec = take(P * 64);
+    L.tiles_touched = take(P * 4);
+    L.depth_keys = take(P * 4);
+    L.clamped = take(P);
+    L.rect = take(P * 8);
+    L.order = take(P * 4);
+    L.order_alt = take(P * 4);
+    L.dkeys_alt = take(P * 4);
+    L.offsets = take(P * 4);
+    L.goff = take(P * 4);
+    size_t hl = hist_len(P);
+    L.hist = take(hl * 4);
+    L.parts = take(scan_parts(hl > P ? hl : P) * 4);
+    L.bytes = o + ALIGN;
+    return L;
+}
+
+// ---- binning buffer (reference BinningState, rasterizer_impl.cu:181-194) ----
+struct BinLayout {
+    size_t tkeys, tkeys_alt, vals_alt, slot_vals, slot_gid, point_list, hist, parts, bytes;
+};
+inline BinLayout bin_layout(size_t I) {
+    BinLayout L{};
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes); return r; };
+    L.tkeys = take(I * 4);
+    L.tkeys_alt = take(I * 4);
+    L.vals_alt = take(I * 4);
+    L.slot_vals = take(I * 4);
+    L.slot_gid = take(I * 4);
+    L.point_list = take(I * 4);
+    size_t hl = hist_len(I);
+    L.hist = take(hl * 4);
+    L.parts = take(scan_parts(hl) * 4);
+    L.bytes = o + ALIGN;
+    return L;
+}
+
+// ---- image buffer (reference ImageState, rasterizer_impl.cu:173-179) ----
+struct ImgLayout {
+    size_t ranges, n_contrib, bytes;
+    int gx, gy;
+};
+inline ImgLayout img_layout(int W, int H) {
+    ImgLayout L{};
+    L.gx = (W + BX - 1) / BX;
+    L.gy = (H + BY - 1) / BY;
+    size_t T = (size_t)L.gx * L.gy;
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes); return r; };
+    L.ranges = take(T * 8);
+    L.n_contrib = take(T * TILE_PIX * 4);  // tile-major: [tile][local pixel]
+    L.bytes = o + ALIGN;
+    return L;
+}
+
+inline char* aligned_base(void* p) {
+    uintptr_t u = reinterpret_cast<uintptr_t>(p);
+    return reinterpret_cast<char*>((u + ALIGN - 1) & ~(uintptr_t)(ALIGN - 1));
+}
+
+// ---- launchers (defined in the .hip files) ----
+// preprocess.hip
+void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec,
+                       int* radii, uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped,
+                       ushort4* rect, hipStream_t st);
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
+void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
+                              const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
+                              const float* contrib, const gsr_grads& g, hipStream_t st);
+// binning.hip
+void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL = identity*/, uint32_t* keys_tmp,
+                       uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,
+                       uint32_t* hist, uint32_t* parts, hipStream_t st);
+void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
+                                  uint32_t* parts, hipStream_t st);
+void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
+                      const ushort4* rect, int gx, uint32_t* tkeys, uint32_t* slot_gid, uint32_t* goff,
+                      hipStream_t st);
+void launch_finalize(size_t I, const uint32_t* tkeys, const uint32_t* slot_vals, const uint32_t* slot_gid,
+                     uint32_t* point_list, uint2* ranges, hipStream_t st);
+// render.hip
+void launch_render_forward(int W, int H, int gx, int gy, const uint2* ranges, const uint32_t* point_list,
+                           const float4* rec, const float* bg, float* out_color, float* out_depth,
+                           float* out_alpha, float* out_segment, uint32_t* n_contrib, hipStream_t st);
+void launch_render_backward(int W, int H, int gx, int gy, const uint2* ranges, const uint32_t* point_list,
+                            const uint32_t* slot_vals, const float4* rec, const float* bg, const float* alpha,
+                            const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_dsegment,
+                            const float* dL_ddepth, const float* dL_dalpha, float* contrib, hipStream_t st);
+
+uint32_t higher_msb(uint32_t n);
+
+}  // namespace gsr

@@ -1,0 +1,562 @@
+// preprocess.hip -- per-Gaussian kernels: forward preprocess (projection, EWA
+// covariance, SH colour, tile rectangle), frustum visibility, and the fused
+// per-Gaussian backward (instance-gradient gather + computeCov2DCUDA +
+// preprocessCUDA backward of the reference).
+//
+// Reference: DGR/cuda_rasterizer/forward.cu:18-256, backward.cu:18-412,
+// auxiliary.h:41-164, rasterizer_impl.cu:54-66.
+//
+// FP contraction is OFF in this file: every product/sum is rounded as written,
+// in the reference's (glm's) evaluation order.  Division and sqrt are IEEE
+// correctly rounded (hipcc default -fhip-fp32-correctly-rounded-divide-sqrt),
+// ndc2Pix runs in double.  With the same choices in the CPU oracle, radii,
+// tiles_touched, depth bits, rectangles and therefore every key, point_list and
+// range are bit-identical to the oracle.
+#pragma clang fp contract(off)
+
+#include "gsr_internal.h"
+
+namespace gsr {
+namespace {
+
+// auxiliary.h:21-39
+__constant__ float C_SH0 = 0.28209479177387814f;
+__constant__ float C_SH1 = 0.4886025119029199f;
+__constant__ float C_SH2[5] = {1.0925484305920792f, -1.0925484305920792f, 0.31539156525252005f,
+                               -1.0925484305920792f, 0.5462742152960396f};
+__constant__ float C_SH3[7] = {-0.5900435899266435f, 2.890611442640554f, -0.4570457994644658f,
+                               0.3731763325901154f, -0.4570457994644658f, 1.445305721320277f,
+                               -0.5900435899266435f};
+
+struct f3 { float x, y, z; };
+__device__ __forceinline__ f3 operator+(f3 a, f3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+__device__ __forceinline__ f3 operator-(f3 a, f3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+__device__ __forceinline__ f3 operator*(float s, f3 a) { return {s * a.x, s * a.y, s * a.z}; }
+__device__ __forceinline__ f3 operator*(f3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+__device__ __forceinline__ f3 operator/(f3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
+__device__ __forceinline__ float dot3(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+
+// Column-major 3x3 with glm semantics: m[col][row].
+struct M3 { float m[3][3]; };
+__device__ __forceinline__ M3 mat3(float a, float b, float c, float d, float e, float f, float g, float h,
+                                   float i) {
+    M3 r;
+    r.m[0][0] = a; r.m[0][1] = b; r.m[0][2] = c;
+    r.m[1][0] = d; r.m[1][1] = e; r.m[1][2] = f;
+    r.m[2][0] = g; r.m[2][1] = h; r.m[2][2] = i;
+    return r;
+}
+// glm operator*(mat3, mat3): R[c][r] = A[0][r]*B[c][0] + A[1][r]*B[c][1] + A[2][r]*B[c][2]
+__device__ __forceinline__ M3 mmul(const M3& A, const M3& B) {
+    M3 R;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r)
+            R.m[c][r] = A.m[0][r] * B.m[c][0] + A.m[1][r] * B.m[c][1] + A.m[2][r] * B.m[c][2];
+    return R;
+}
+__device__ __forceinline__ M3 mtr(const M3& A) {
+    M3 R;
+#pragma unroll
+    for (int c = 0; c < 3; ++c)
+#pragma unroll
+        for (int r = 0; r < 3; ++r) R.m[c][r] = A.m[r][c];
+    return R;
+}
+
+__device__ __forceinline__ f3 xform4x3(f3 p, const float* m) {
+    return {m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+            m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]};
+}
+__device__ __forceinline__ float4 xform4x4(f3 p, const float* m) {
+    return {m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12], m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
+            m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14], m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]};
+}
+__device__ __forceinline__ f3 xformVecT(f3 p, const float* m) {
+    return {m[0] * p.x + m[1] * p.y + m[2] * p.z, m[4] * p.x + m[5] * p.y + m[6] * p.z,
+            m[8] * p.x + m[9] * p.y + m[10] * p.z};
+}
+
+// auxiliary.h:41-44
+__device__ __forceinline__ float ndc2pix(float v, int S) { return (float)(((v + 1.0) * S - 1.0) * 0.5); }
+
+// auxiliary.h:46-56
+__device__ __forceinline__ void get_rect(float px, float py, int r, int gx, int gy, int& x0, int& y0, int& x1,
+                                         int& y1) {
+    x0 = min(gx, max(0, (int)((px - (float)r) / (float)BX)));
+    y0 = min(gy, max(0, (int)((py - (float)r) / (float)BY)));
+    x1 = min(gx, max(0, (int)((((px + (float)r) + (float)BX) - 1.0f) / (float)BX)));
+    y1 = min(gy, max(0, (int)((((py + (float)r) + (float)BY) - 1.0f) / (float)BY)));
+}
+
+__device__ __forceinline__ f3 ld3(const float* p) { return {p[0], p[1], p[2]}; }
+
+// forward.cu:118-152 (quaternion used as given: normalised upstream)
+__device__ __forceinline__ void cov3d_from(f3 scale, float mod, float4 q, float c[6]) {
+    M3 S = mat3(1, 0, 0, 0, 1, 0, 0, 0, 1);
+    S.m[0][0] = mod * scale.x;
+    S.m[1][1] = mod * scale.y;
+    S.m[2][2] = mod * scale.z;
+    const float r = q.x, x = q.y, y = q.z, z = q.w;
+    M3 R = mat3(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+    M3 Mm = mmul(S, R);
+    M3 Sig = mmul(mtr(Mm), Mm);
+    c[0] = Sig.m[0][0]; c[1] = Sig.m[0][1]; c[2] = Sig.m[0][2];
+    c[3] = Sig.m[1][1]; c[4] = Sig.m[1][2]; c[5] = Sig.m[2][2];
+}
+
+// Clamped camera-space mean, J, W, T of forward.cu:80-99 / backward.cu:166-192.
+struct EwaTerms { f3 t; float txtz, tytz, limx, limy; M3 W, T; };
+__device__ __forceinline__ EwaTerms ewa_terms(f3 mean, float fx, float fy, float tanx, float tany,
+                                              const float* view) {
+    EwaTerms e;
+    f3 t = xform4x3(mean, view);
+    e.limx = 1.3f * tanx;
+    e.limy = 1.3f * tany;
+    e.txtz = t.x / t.z;
+    e.tytz = t.y / t.z;
+    t.x = fminf(e.limx, fmaxf(-e.limx, e.txtz)) * t.z;
+    t.y = fminf(e.limy, fmaxf(-e.limy, e.tytz)) * t.z;
+    e.t = t;
+    M3 J = mat3(fx / t.z, 0.0f, -(fx * t.x) / (t.z * t.z), 0.0f, fy / t.z, -(fy * t.y) / (t.z * t.z), 0, 0, 0);
+    e.W = mat3(view[0], view[4], view[8], view[1], view[5], view[9], view[2], view[6], view[10]);
+    e.T = mmul(e.W, J);
+    return e;
+}
+
+__device__ __forceinline__ M3 vrk_of(const float* c) {
+    return mat3(c[0], c[1], c[2], c[1], c[3], c[4], c[2], c[4], c[5]);
+}
+
+// forward.cu:20-71: RGB from SH (deg <= 3), +0.5, clamp >= 0, record clamping.
+__device__ __forceinline__ f3 color_from_sh(int deg, f3 dir, const float* sh, uint8_t& clamp_bits) {
+    auto S = [&](int i) { return ld3(sh + 3 * i); };
+    f3 result = C_SH0 * S(0);
+    if (deg > 0) {
+        const float x = dir.x, y = dir.y, z = dir.z;
+        result = result - C_SH1 * y * S(1) + C_SH1 * z * S(2) - C_SH1 * x * S(3);
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z;
+            const float xy = x * y, yz = y * z, xz = x * z;
+            result = result + C_SH2[0] * xy * S(4) + C_SH2[1] * yz * S(5) +
+                     C_SH2[2] * (2.0f * zz - xx - yy) * S(6) + C_SH2[3] * xz * S(7) +
+                     C_SH2[4] * (xx - yy) * S(8);
+            if (deg > 2) {
+                result = result + C_SH3[0] * y * (3.0f * xx - yy) * S(9) + C_SH3[1] * xy * z * S(10) +
+                         C_SH3[2] * y * (4.0f * zz - xx - yy) * S(11) +
+                         C_SH3[3] * z * (2.0f * zz - 3.0f * xx - 3.0f * yy) * S(12) +
+                         C_SH3[4] * x * (4.0f * zz - xx - yy) * S(13) + C_SH3[5] * z * (xx - yy) * S(14) +
+                         C_SH3[6] * x * (xx - 3.0f * yy) * S(15);
+            }
+        }
+    }
+    result = result + f3{0.5f, 0.5f, 0.5f};
+    clamp_bits = (uint8_t)((result.x < 0 ? 1 : 0) | (result.y < 0 ? 2 : 0) | (result.z < 0 ? 4 : 0));
+    return {fmaxf(result.x, 0.0f), fmaxf(result.y, 0.0f), fmaxf(result.z, 0.0f)};
+}
+
+struct Cam {
+    float view[16], proj[16];
+    f3 campos;
+};
+
+// Camera matrices live in device memory (the reference passes CUDA tensors);
+// one uniform load per wave through the scalar cache.
+__device__ __forceinline__ void load_cam(const gsr_settings& s, Cam& c) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { c.view[i] = s.viewmatrix[i]; c.proj[i] = s.projmatrix[i]; }
+    c.campos = ld3(s.campos);
+}
+
+// ------------------------------------------------------------------ forward --
+// preprocessCUDA (forward.cu:154-256).  One thread per Gaussian.
+__global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs in, int gx, int gy,
+                                                    float4* __restrict__ rec, int* __restrict__ radii,
+                                                    uint32_t* __restrict__ tiles_touched,
+                                                    uint32_t* __restrict__ depth_keys,
+                                                    uint8_t* __restrict__ clamped, ushort4* __restrict__ rect) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= s.P) return;
+    Cam cam;
+    load_cam(s, cam);
+    radii[idx] = 0;
+    tiles_touched[idx] = 0;
+    depth_keys[idx] = 0xFFFFFFFFu;  // culled Gaussians sort last; they emit no instances
+    clamped[idx] = 0;
+
+    const f3 p_orig = ld3(in.means3D + 3 * (size_t)idx);
+    // in_frustum (auxiliary.h:139-164)
+    const f3 p_view = xform4x3(p_orig, cam.view);
+    if (p_view.z <= 0.2f) return;
+    const float4 p_hom = xform4x4(p_orig, cam.proj);
+    const float p_w = 1.0f / (p_hom.w + 0.0000001f);
+    const f3 p_proj = {p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w};
+
+    float c3[6];
+    if (in.cov3D_precomp) {
+        const float* c = in.cov3D_precomp + 6 * (size_t)idx;
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c3[i] = c[i];
+    } else {
+        const float4 q = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)idx);
+        cov3d_from(ld3(in.scales + 3 * (size_t)idx), s.scale_modifier, q, c3);
+    }
+    const float focal_y = s.H / (2.0f * s.tanfovy);
+    const float focal_x = s.W / (2.0f * s.tanfovx);
+    const EwaTerms e = ewa_terms(p_orig, focal_x, focal_y, s.tanfovx, s.tanfovy, cam.view);
+    const M3 cov = mmul(mmul(mtr(e.T), mtr(vrk_of(c3))), e.T);
+    const float cx = cov.m[0][0] + 0.3f, cy = cov.m[0][1], cz = cov.m[1][1] + 0.3f;
+
+    const float det = (cx * cz - cy * cy);
+    if (det == 0.0f) return;
+    const float det_inv = 1.f / det;
+    const float conic_x = cz * det_inv, conic_y = -cy * det_inv, conic_z = cx * det_inv;
+    const float mid = 0.5f * (cx + cz);
+    const float lambda1 = mid + sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
+    const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
+    const float px = ndc2pix(p_proj.x, s.W), py = ndc2pix(p_proj.y, s.H);
+    int x0, y0, x1, y1;
+    get_rect(px, py, (int)my_radius, gx, gy, x0, y0, x1, y1);
+    const uint32_t ntiles = (uint32_t)((x1 - x0) * (y1 - y0));
+    if (ntiles == 0) return;
+
+    f3 rgb;
+    uint8_t cbits = 0;
+    if (in.colors_precomp == nullptr) {
+        f3 dir = p_orig - cam.campos;
+        dir = dir / sqrtf(dot3(dir, dir));
+        rgb = color_from_sh(s.D, dir, in.shs + (size_t)idx * s.M * 3, cbits);
+    } else {
+        rgb = ld3(in.colors_precomp + 3 * (size_t)idx);
+    }
+    float s0 = 0.f, s1 = 0.f;
+    if (in.segments) {
+        const float2 sg = *reinterpret_cast<const float2*>(in.segments + 2 * (size_t)idx);
+        s0 = sg.x;
+        s1 = sg.y;
+    }
+    const float opacity = in.opacities[idx];
+    float4* R = rec + (size_t)idx * REC_F4;
+    R[0] = make_float4(px, py, conic_x, conic_y);
+    R[1] = make_float4(conic_z, opacity, p_view.z, s0);
+    R[2] = make_float4(rgb.x, rgb.y, rgb.z, s1);
+    R[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    radii[idx] = (int)my_radius;
+    tiles_touched[idx] = ntiles;
+    depth_keys[idx] = __float_as_uint(p_view.z);
+    clamped[idx] = cbits;
+    rect[idx] = make_ushort4((unsigned short)x0, (unsigned short)y0, (unsigned short)x1, (unsigned short)y1);
+}
+
+// checkFrustum (rasterizer_impl.cu:54-66)
+__global__ void k_mark_visible(int P, const float* __restrict__ means3D, const float* __restrict__ view,
+                               uint8_t* __restrict__ present) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    float v[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) v[i] = view[i];
+    present[idx] = xform4x3(ld3(means3D + 3 * (size_t)idx), v).z > 0.2f ? 1 : 0;
+}
+
+// ----------------------------------------------------------------- backward --
+// One thread per Gaussian.  Sums the per-(tile, Gaussian) gradient records that
+// the render backward wrote at the Gaussian's instance slots (replacing the
+// reference's 12 per-pixel atomicAdds, backward.cu:575-636), then runs
+// computeCov2DCUDA (backward.cu:141-274) and preprocessCUDA backward
+// (backward.cu:343-412) on the sums.  Record layout (12 floats):
+//   [dcolor.rgb, dseg0, dseg1, ddepth, dmean2D.x, dmean2D.y, dconic.x, dconic.y, dconic.w, dopacity]
+__global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_inputs in,
+                                                           const int* __restrict__ radii,
+                                                           const uint32_t* __restrict__ tiles_touched,
+                                                           const uint32_t* __restrict__ goff,
+                                                           const uint8_t* __restrict__ clamped,
+                                                           const float* __restrict__ contrib, gsr_grads g) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= s.P) return;
+    const int M = s.M;
+    const size_t i3 = 3 * (size_t)idx;
+    if (!(radii[idx] > 0)) {
+        // invisible: every gradient is zero (rasterize_points.cu:166-177 zero-init)
+        if (g.dmeans2D) { g.dmeans2D[i3] = 0.f; g.dmeans2D[i3 + 1] = 0.f; g.dmeans2D[i3 + 2] = 0.f; }
+        if (g.dcolors) { g.dcolors[i3] = 0.f; g.dcolors[i3 + 1] = 0.f; g.dcolors[i3 + 2] = 0.f; }
+        if (g.dopacity) g.dopacity[idx] = 0.f;
+        if (g.dmeans3D) { g.dmeans3D[i3] = 0.f; g.dmeans3D[i3 + 1] = 0.f; g.dmeans3D[i3 + 2] = 0.f; }
+        if (g.dcov3D) for (int i = 0; i < 6; ++i) g.dcov3D[6 * (size_t)idx + i] = 0.f;
+        if (g.dsh && in.shs) for (int i = 0; i < 3 * M; ++i) g.dsh[(size_t)idx * 3 * M + i] = 0.f;
+        if (g.dscales && in.scales) { g.dscales[i3] = 0.f; g.dscales[i3 + 1] = 0.f; g.dscales[i3 + 2] = 0.f; }
+        if (g.drot && in.scales) for (int i = 0; i < 4; ++i) g.drot[4 * (size_t)idx + i] = 0.f;
+        if (g.dsegments) { g.dsegments[2 * (size_t)idx] = 0.f; g.dsegments[2 * (size_t)idx + 1] = 0.f; }
+        return;
+    }
+    // gather-sum of the instance records, in slot order (deterministic)
+    float q[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) q[j] = 0.f;
+    {
+        const uint32_t n = tiles_touched[idx];
+        const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)goff[idx] * 12);
+        for (uint32_t k = 0; k < n; ++k) {
+            const float4 a = src[3 * k], b = src[3 * k + 1], c = src[3 * k + 2];
+            q[0] += a.x; q[1] += a.y; q[2] += a.z; q[3] += a.w;
+            q[4] += b.x; q[5] += b.y; q[6] += b.z; q[7] += b.w;
+            q[8] += c.x; q[9] += c.y; q[10] += c.z; q[11] += c.w;
+        }
+    }
+    if (g.dmeans2D) { g.dmeans2D[i3] = q[6]; g.dmeans2D[i3 + 1] = q[7]; g.dmeans2D[i3 + 2] = 0.f; }
+    if (g.dcolors) { g.dcolors[i3] = q[0]; g.dcolors[i3 + 1] = q[1]; g.dcolors[i3 + 2] = q[2]; }
+    if (g.dopacity) g.dopacity[idx] = q[11];
+    if (g.dsegments) { g.dsegments[2 * (size_t)idx] = q[3]; g.dsegments[2 * (size_t)idx + 1] = q[4]; }
+
+    Cam cam;
+    load_cam(s, cam);
+    const float focal_y = s.H / (2.0f * s.tanfovy);
+    const float focal_x = s.W / (2.0f * s.tanfovx);
+    const f3 mean = ld3(in.means3D + i3);
+
+    // ---- computeCov2DCUDA (backward.cu:155-273)
+    float c3[6];
+    float4 quat = make_float4(0.f, 0.f, 0.f, 0.f);
+    f3 scale = {0.f, 0.f, 0.f};
+    if (in.cov3D_precomp) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c3[i] = in.cov3D_precomp[6 * (size_t)idx + i];
+    } else {
+        quat = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)idx);
+        scale = ld3(in.scales + i3);
+        cov3d_from(scale, s.scale_modifier, quat, c3);  // == the forward's geom.cov3D
+    }
+    const float dcx = q[8], dcy = q[9], dcz = q[10];
+    const EwaTerms e = ewa_terms(mean, focal_x, focal_y, s.tanfovx, s.tanfovy, cam.view);
+    const float x_grad_mul = e.txtz < -e.limx || e.txtz > e.limx ? 0 : 1;
+    const float y_grad_mul = e.tytz < -e.limy || e.tytz > e.limy ? 0 : 1;
+    const M3 Vrk = vrk_of(c3);
+    const M3& T = e.T;
+    const M3 cov2D = mmul(mmul(mtr(T), mtr(Vrk)), T);
+    const float a = cov2D.m[0][0] + 0.3f;
+    const float b = cov2D.m[0][1];
+    const float c = cov2D.m[1][1] + 0.3f;
+    const float denom = a * c - b * b;
+    float dL_da = 0, dL_db = 0, dL_dc = 0;
+    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+    float dcv[6] = {0, 0, 0, 0, 0, 0};
+    const auto& Tt = T.m;
+    if (denom2inv != 0) {
+        dL_da = denom2inv * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
+        dL_dc = denom2inv * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
+        dL_db = denom2inv * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
+        dcv[0] = (Tt[0][0] * Tt[0][0] * dL_da + Tt[0][0] * Tt[1][0] * dL_db + Tt[1][0] * Tt[1][0] * dL_dc);
+        dcv[3] = (Tt[0][1] * Tt[0][1] * dL_da + Tt[0][1] * Tt[1][1] * dL_db + Tt[1][1] * Tt[1][1] * dL_dc);
+        dcv[5] = (Tt[0][2] * Tt[0][2] * dL_da + Tt[0][2] * Tt[1][2] * dL_db + Tt[1][2] * Tt[1][2] * dL_dc);
+        dcv[1] = 2 * Tt[0][0] * Tt[0][1] * dL_da + (Tt[0][0] * Tt[1][1] + Tt[0][1] * Tt[1][0]) * dL_db +
+                 2 * Tt[1][0] * Tt[1][1] * dL_dc;
+        dcv[2] = 2 * Tt[0][0] * Tt[0][2] * dL_da + (Tt[0][0] * Tt[1][2] + Tt[0][2] * Tt[1][0]) * dL_db +
+                 2 * Tt[1][0] * Tt[1][2] * dL_dc;
+        dcv[4] = 2 * Tt[0][2] * Tt[0][1] * dL_da + (Tt[0][1] * Tt[1][2] + Tt[0][2] * Tt[1][1]) * dL_db +
+                 2 * Tt[1][1] * Tt[1][2] * dL_dc;
+    }
+    const auto& V = Vrk.m;
+    const float dL_dT00 = 2 * (Tt[0][0] * V[0][0] + Tt[0][1] * V[0][1] + Tt[0][2] * V[0][2]) * dL_da +
+                          (Tt[1][0] * V[0][0] + Tt[1][1] * V[0][1] + Tt[1][2] * V[0][2]) * dL_db;
+    const float dL_dT01 = 2 * (Tt[0][0] * V[1][0] + Tt[0][1] * V[1][1] + Tt[0][2] * V[1][2]) * dL_da +
+                          (Tt[1][0] * V[1][0] + Tt[1][1] * V[1][1] + Tt[1][2] * V[1][2]) * dL_db;
+    const float dL_dT02 = 2 * (Tt[0][0] * V[2][0] + Tt[0][1] * V[2][1] + Tt[0][2] * V[2][2]) * dL_da +
+                          (Tt[1][0] * V[2][0] + Tt[1][1] * V[2][1] + Tt[1][2] * V[2][2]) * dL_db;
+    const float dL_dT10 = 2 * (Tt[1][0] * V[0][0] + Tt[1][1] * V[0][1] + Tt[1][2] * V[0][2]) * dL_dc +
+                          (Tt[0][0] * V[0][0] + Tt[0][1] * V[0][1] + Tt[0][2] * V[0][2]) * dL_db;
+    const float dL_dT11 = 2 * (Tt[1][0] * V[1][0] + Tt[1][1] * V[1][1] + Tt[1][2] * V[1][2]) * dL_dc +
+                          (Tt[0][0] * V[1][0] + Tt[0][1] * V[1][1] + Tt[0][2] * V[1][2]) * dL_db;
+    const float dL_dT12 = 2 * (Tt[1][0] * V[2][0] + Tt[1][1] * V[2][1] + Tt[1][2] * V[2][2]) * dL_dc +
+                          (Tt[0][0] * V[2][0] + Tt[0][1] * V[2][1] + Tt[0][2] * V[2][2]) * dL_db;
+    const auto& Wt = e.W.m;
+    const float dL_dJ00 = Wt[0][0] * dL_dT00 + Wt[0][1] * dL_dT01 + Wt[0][2] * dL_dT02;
+    const float dL_dJ02 = Wt[2][0] * dL_dT00 + Wt[2][1] * dL_dT01 + Wt[2][2] * dL_dT02;
+    const float dL_dJ11 = Wt[1][0] * dL_dT10 + Wt[1][1] * dL_dT11 + Wt[1][2] * dL_dT12;
+    const float dL_dJ12 = Wt[2][0] * dL_dT10 + Wt[2][1] * dL_dT11 + Wt[2][2] * dL_dT12;
+    const float hx = focal_x, hy = focal_y;
+    const f3 t = e.t;
+    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+    const float dL_dtx = x_grad_mul * -hx * tz2 * dL_dJ02;
+    const float dL_dty = y_grad_mul * -hy * tz2 * dL_dJ12;
+    const float dL_dtz = -hx * tz2 * dL_dJ00 - hy * tz2 * dL_dJ11 + (2 * hx * t.x) * tz3 * dL_dJ02 +
+                         (2 * hy * t.y) * tz3 * dL_dJ12;
+    f3 dmean = xformVecT({dL_dtx, dL_dty, dL_dtz}, cam.view);
+    if (g.dcov3D)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) g.dcov3D[6 * (size_t)idx + i] = dcv[i];
+
+    // ---- preprocessCUDA backward (backward.cu:372-411)
+    const float* proj = cam.proj;
+    const float* view = cam.view;
+    const f3 m = mean;
+    const float4 m_hom = xform4x4(m, proj);
+    const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+    const float d2x = q[6], d2y = q[7];
+    const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+    const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+    f3 dm;
+    dm.x = (proj[0] * m_w - proj[3] * mul1) * d2x + (proj[1] * m_w - proj[3] * mul2) * d2y;
+    dm.y = (proj[4] * m_w - proj[7] * mul1) * d2x + (proj[5] * m_w - proj[7] * mul2) * d2y;
+    dm.z = (proj[8] * m_w - proj[11] * mul1) * d2x + (proj[9] * m_w - proj[11] * mul2) * d2y;
+    dmean = dmean + dm;
+    const float ddepth = q[5];
+    const float mul3 = view[2] * m.x + view[6] * m.y + view[10] * m.z + view[14];
+    f3 dm2;
+    dm2.x = (view[2] - view[3] * mul3) * ddepth;
+    dm2.y = (view[6] - view[7] * mul3) * ddepth;
+    dm2.z = (view[10] - view[11] * mul3) * ddepth;
+    dmean = dmean + dm2;
+
+    if (in.shs) {
+        // computeColorFromSH backward (backward.cu:20-139)
+        const int deg = s.D;
+        const float* shp = in.shs + (size_t)idx * M * 3;
+        auto S = [&](int i) { return ld3(shp + 3 * i); };
+        const f3 dir_orig = m - cam.campos;
+        const f3 dir = dir_orig / sqrtf(dot3(dir_orig, dir_orig));
+        const uint8_t cb = clamped[idx];
+        f3 dRGB = {q[0], q[1], q[2]};
+        dRGB.x *= (cb & 1) ? 0 : 1;
+        dRGB.y *= (cb & 2) ? 0 : 1;
+        dRGB.z *= (cb & 4) ? 0 : 1;
+        f3 dx = {0, 0, 0}, dy = {0, 0, 0}, dz = {0, 0, 0};
+        const float x = dir.x, y = dir.y, z = dir.z;
+        float* o = g.dsh ? g.dsh + (size_t)idx * M * 3 : nullptr;
+        auto put = [&](int i, f3 v) {
+            if (o) { o[3 * i] = v.x; o[3 * i + 1] = v.y; o[3 * i + 2] = v.z; }
+        };
+        put(0, C_SH0 * dRGB);
+        int ncoef = 1;
+        if (deg > 0) {
+            ncoef = 4;
+            const float s1 = -C_SH1 * y, s2 = C_SH1 * z, s3 = -C_SH1 * x;
+            put(1, s1 * dRGB); put(2, s2 * dRGB); put(3, s3 * dRGB);
+            dx = -C_SH1 * S(3);
+            dy = -C_SH1 * S(1);
+            dz = C_SH1 * S(2);
+            if (deg > 1) {
+                ncoef = 9;
+                const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                put(4, (C_SH2[0] * xy) * dRGB);
+                put(5, (C_SH2[1] * yz) * dRGB);
+                put(6, (C_SH2[2] * (2.f * zz - xx - yy)) * dRGB);
+                put(7, (C_SH2[3] * xz) * dRGB);
+                put(8, (C_SH2[4] * (xx - yy)) * dRGB);
+                dx = dx + (C_SH2[0] * y * S(4) + C_SH2[2] * 2.f * -x * S(6) + C_SH2[3] * z * S(7) +
+                           C_SH2[4] * 2.f * x * S(8));
+                dy = dy + (C_SH2[0] * x * S(4) + C_SH2[1] * z * S(5) + C_SH2[2] * 2.f * -y * S(6) +
+                           C_SH2[4] * 2.f * -y * S(8));
+                dz = dz + (C_SH2[1] * y * S(5) + C_SH2[2] * 2.f * 2.f * z * S(6) + C_SH2[3] * x * S(7));
+                if (deg > 2) {
+                    ncoef = 16;
+                    put(9, (C_SH3[0] * y * (3.f * xx - yy)) * dRGB);
+                    put(10, (C_SH3[1] * xy * z) * dRGB);
+                    put(11, (C_SH3[2] * y * (4.f * zz - xx - yy)) * dRGB);
+                    put(12, (C_SH3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy)) * dRGB);
+                    put(13, (C_SH3[4] * x * (4.f * zz - xx - yy)) * dRGB);
+                    put(14, (C_SH3[5] * z * (xx - yy)) * dRGB);
+                    put(15, (C_SH3[6] * x * (xx - 3.f * yy)) * dRGB);
+                    dx = dx + (C_SH3[0] * S(9) * 3.f * 2.f * xy + C_SH3[1] * S(10) * yz +
+                               C_SH3[2] * S(11) * -2.f * xy + C_SH3[3] * S(12) * -3.f * 2.f * xz +
+                               C_SH3[4] * S(13) * (-3.f * xx + 4.f * zz - yy) + C_SH3[5] * S(14) * 2.f * xz +
+                               C_SH3[6] * S(15) * 3.f * (xx - yy));
+                    dy = dy + (C_SH3[0] * S(9) * 3.f * (xx - yy) + C_SH3[1] * S(10) * xz +
+                               C_SH3[2] * S(11) * (-3.f * yy + 4.f * zz - xx) + C_SH3[3] * S(12) * -3.f * 2.f * yz +
+                               C_SH3[4] * S(13) * -2.f * xy + C_SH3[5] * S(14) * -2.f * yz +
+                               C_SH3[6] * S(15) * -3.f * 2.f * xy);
+                    dz = dz + (C_SH3[1] * S(10) * xy + C_SH3[2] * S(11) * 4.f * 2.f * yz +
+                               C_SH3[3] * S(12) * 3.f * (2.f * zz - xx - yy) + C_SH3[4] * S(13) * 4.f * 2.f * xz +
+                               C_SH3[5] * S(14) * (xx - yy));
+                }
+            }
+        }
+        if (o)
+            for (int i = 3 * ncoef; i < 3 * M; ++i) o[i] = 0.f;
+        const f3 dL_ddir = {dot3(dx, dRGB), dot3(dy, dRGB), dot3(dz, dRGB)};
+        // dnormvdv (auxiliary.h:107-117)
+        const f3 v = dir_orig, dv = dL_ddir;
+        const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+        f3 dn;
+        dn.x = ((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32;
+        dn.y = (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32;
+        dn.z = (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32;
+        dmean = dmean + dn;
+    }
+    if (g.dmeans3D) { g.dmeans3D[i3] = dmean.x; g.dmeans3D[i3 + 1] = dmean.y; g.dmeans3D[i3 + 2] = dmean.z; }
+
+    if (in.scales) {
+        // computeCov3D backward (backward.cu:276-341)
+        const float r = quat.x, x = quat.y, y = quat.z, z = quat.w;
+        const M3 R = mat3(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                          2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                          2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+        M3 S = mat3(1, 0, 0, 0, 1, 0, 0, 0, 1);
+        const f3 sv = s.scale_modifier * scale;
+        S.m[0][0] = sv.x;
+        S.m[1][1] = sv.y;
+        S.m[2][2] = sv.z;
+        const M3 Mm = mmul(S, R);
+        const M3 dSig = mat3(dcv[0], 0.5f * dcv[1], 0.5f * dcv[2], 0.5f * dcv[1], dcv[3], 0.5f * dcv[4],
+                             0.5f * dcv[2], 0.5f * dcv[4], dcv[5]);
+        M3 M2;
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc)
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) M2.m[cc][rr] = 2.0f * Mm.m[cc][rr];
+        const M3 dM = mmul(M2, dSig);
+        const M3 Rt = mtr(R);
+        M3 dMt = mtr(dM);
+        if (g.dscales) {
+            g.dscales[i3 + 0] = Rt.m[0][0] * dMt.m[0][0] + Rt.m[0][1] * dMt.m[0][1] + Rt.m[0][2] * dMt.m[0][2];
+            g.dscales[i3 + 1] = Rt.m[1][0] * dMt.m[1][0] + Rt.m[1][1] * dMt.m[1][1] + Rt.m[1][2] * dMt.m[1][2];
+            g.dscales[i3 + 2] = Rt.m[2][0] * dMt.m[2][0] + Rt.m[2][1] * dMt.m[2][1] + Rt.m[2][2] * dMt.m[2][2];
+        }
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+            dMt.m[0][rr] *= sv.x;
+            dMt.m[1][rr] *= sv.y;
+            dMt.m[2][rr] *= sv.z;
+        }
+        const auto& d = dMt.m;
+        if (g.drot) {
+            float* dr = g.drot + 4 * (size_t)idx;
+            dr[0] = 2 * z * (d[0][1] - d[1][0]) + 2 * y * (d[2][0] - d[0][2]) + 2 * x * (d[1][2] - d[2][1]);
+            dr[1] = 2 * y * (d[1][0] + d[0][1]) + 2 * z * (d[2][0] + d[0][2]) + 2 * r * (d[1][2] - d[2][1]) -
+                    4 * x * (d[2][2] + d[1][1]);
+            dr[2] = 2 * x * (d[1][0] + d[0][1]) + 2 * r * (d[2][0] - d[0][2]) + 2 * z * (d[1][2] + d[2][1]) -
+                    4 * y * (d[2][2] + d[0][0]);
+            dr[3] = 2 * r * (d[0][1] - d[1][0]) + 2 * x * (d[2][0] + d[0][2]) + 2 * y * (d[1][2] + d[2][1]) -
+                    4 * z * (d[1][1] + d[0][0]);
+        }
+    }
+}
+
+}  // namespace
+
+void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec, int* radii,
+                       uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped, ushort4* rect,
+                       hipStream_t st) {
+    if (s.P == 0) return;
+    hipLaunchKernelGGL(k_preprocess, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, gx, gy, rec, radii,
+                       tiles_touched, depth_keys, clamped, rect);
+}
+
+void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
+    if (P == 0) return;
+    hipLaunchKernelGGL(k_mark_visible, dim3(cdiv(P, 256)), dim3(256), 0, st, P, means3D, view, present);
+}
+
+void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
+                              const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
+                              const float* contrib, const gsr_grads& g, hipStream_t st) {
+    if (s.P == 0) return;
+    hipLaunchKernelGGL(k_gaussian_backward, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, radii, tiles_touched,
+                       goff, clamped, contrib, g);
+}
+
+}  // namespace gsr

@@ -1,0 +1,310 @@
+"""ctypes binding of libgsr.so (include/gsr.h) with the positional signatures of
+the reference's private extension module `_C` (DGR/ext.cpp:15-19,
+DGR/rasterize_points.h:18-73), so that the public API in __init__.py reads like
+the reference's.
+
+The product path is libgsr.so only: if it is missing, importing this module
+raises ImportError -- there is no CPU or PyTorch fallback.
+"""
+import ctypes
+import os
+
+import torch  # must be imported first: libgsr.so binds to torch's HIP runtime (same soname)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("GSR_LIBRARY", os.path.join(_HERE, "libgsr.so"))
+
+if not os.path.exists(LIB_PATH):
+    raise ImportError(
+        f"libgsr.so not found at {LIB_PATH}; build it with "
+        "`make -C 3d_gaussian_magic_change-segment_3dgs_amd/csrc` (or __graft_entry__.build())")
+
+_lib = ctypes.CDLL(LIB_PATH)
+
+NUM_CHANNELS = 3  # config.h:15
+NUM_CLASS = 2     # config.h:16
+
+
+class _Settings(ctypes.Structure):
+    _fields_ = [
+        ("P", ctypes.c_int), ("D", ctypes.c_int), ("M", ctypes.c_int), ("W", ctypes.c_int), ("H", ctypes.c_int),
+        ("tanfovx", ctypes.c_float), ("tanfovy", ctypes.c_float), ("scale_modifier", ctypes.c_float),
+        ("prefiltered", ctypes.c_int), ("debug", ctypes.c_int),
+        ("bg", ctypes.c_void_p), ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
+        ("campos", ctypes.c_void_p),
+    ]
+
+
+class _Inputs(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "means3D", "shs", "colors_precomp", "segments", "opacities", "scales", "rotations", "cov3D_precomp")]
+
+
+class _Grads(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in (
+        "dmeans2D", "dcolors", "dopacity", "dmeans3D", "dcov3D", "dsh", "dscales", "drot", "dsegments")]
+
+
+_vp, _i, _sz = ctypes.c_void_p, ctypes.c_int, ctypes.c_size_t
+_lib.gsr_geom_bytes.restype = _sz
+_lib.gsr_geom_bytes.argtypes = [_i]
+_lib.gsr_binning_bytes.restype = _sz
+_lib.gsr_binning_bytes.argtypes = [_i]
+_lib.gsr_img_bytes.restype = _sz
+_lib.gsr_img_bytes.argtypes = [_i, _i]
+_lib.gsr_backward_scratch_bytes.restype = _sz
+_lib.gsr_backward_scratch_bytes.argtypes = [_i]
+_lib.gsr_forward_geometry.restype = _i
+_lib.gsr_forward_geometry.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _vp, _vp, _vp,
+                                      ctypes.POINTER(ctypes.c_int)]
+_lib.gsr_forward_render.restype = _i
+_lib.gsr_forward_render.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _vp, _vp, _vp, _i,
+                                    _vp, _vp, _vp, _vp, _vp]
+_lib.gsr_backward.restype = _i
+_lib.gsr_backward.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _vp, _vp, _vp, _vp, _i, _vp,
+                              _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_Grads), _vp]
+_lib.gsr_mark_visible.restype = _i
+_lib.gsr_mark_visible.argtypes = [_i, _vp, _vp, _vp, _vp, _vp]
+_lib.gsr_last_error.restype = ctypes.c_char_p
+_lib.gsr_version.restype = ctypes.c_char_p
+_lib.gsr_debug_copy.restype = ctypes.c_longlong
+_lib.gsr_debug_copy.argtypes = [ctypes.c_char_p, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]
+
+EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_img_bytes", "gsr_backward_scratch_bytes",
+                    "gsr_forward_geometry", "gsr_forward_render", "gsr_backward", "gsr_mark_visible",
+                    "gsr_debug_copy", "gsr_last_error", "gsr_version")
+
+_DEBUG_FIELDS = {  # name -> (dtype, elements per unit, unit: P | I | T)
+    "tiles_touched": (torch.int32, 1, "P"), "rec": (torch.float32, 16, "P"), "clamped": (torch.uint8, 1, "P"),
+    "order": (torch.int32, 1, "P"), "goff": (torch.int32, 1, "P"), "point_list": (torch.int32, 1, "I"),
+    "slot_vals": (torch.int32, 1, "I"), "ranges": (torch.int32, 2, "T"), "n_contrib_tiles": (torch.int32, 256, "T"),
+}
+
+
+def debug_state(name, P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffer):
+    """Copy of one private intermediate of a forward call (parity tests only; see
+    gsr_debug_copy in include/gsr.h).  Unsigned arrays are returned as int32."""
+    dtype, per, unit = _DEBUG_FIELDS[name]
+    T = ((W + 15) // 16) * ((H + 15) // 16)
+    n = {"P": P, "I": num_rendered, "T": T}[unit] * per
+    dev = geomBuffer.device
+    out = torch.empty(max(n, 1), dtype=dtype, device=dev)
+    ptr = lambda t: t.data_ptr() if t is not None and t.numel() else None
+    rc = _lib.gsr_debug_copy(name.encode(), P, W, H, num_rendered, ptr(geomBuffer), ptr(binningBuffer),
+                             ptr(imgBuffer), out.data_ptr(), _stream(dev))
+    if rc < 0:
+        raise RuntimeError(f"gsr_debug_copy({name}) failed: {_lib.gsr_last_error().decode()}")
+    return out[:n]
+
+
+def version():
+    return _lib.gsr_version().decode()
+
+
+def _check(rc):
+    if rc != 0:
+        raise RuntimeError(_lib.gsr_last_error().decode())
+
+
+def _present(t):
+    return isinstance(t, torch.Tensor) and t.numel() > 0
+
+
+def _dev_f32(t, device, name, align=4):
+    """Contiguous fp32 tensor on `device` (reference: .contiguous().data<float>()),
+    re-allocated if its address is not `align`-aligned for vector loads."""
+    if not _present(t):
+        return None
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be a float32 tensor (got {t.dtype})")
+    if t.device != device:
+        if t.device.type != "cpu":
+            raise RuntimeError(f"{name} is on {t.device}, expected {device}")
+        t = t.to(device)
+    t = t.contiguous()
+    if t.data_ptr() % align:
+        t = t.clone()
+    return t
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(device):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def _settings(P, D, M, W, H, tanfovx, tanfovy, scale_modifier, prefiltered, debug, bg, view, proj, campos):
+    s = _Settings()
+    s.P, s.D, s.M, s.W, s.H = P, D, M, W, H
+    s.tanfovx, s.tanfovy, s.scale_modifier = float(tanfovx), float(tanfovy), float(scale_modifier)
+    s.prefiltered, s.debug = int(bool(prefiltered)), int(bool(debug))
+    s.bg, s.viewmatrix, s.projmatrix, s.campos = _ptr(bg), _ptr(view), _ptr(proj), _ptr(campos)
+    return s
+
+
+def _inputs(means3D, sh, colors, segments, opacity, scales, rotations, cov3D_precomp):
+    i = _Inputs()
+    i.means3D, i.shs, i.colors_precomp, i.segments = _ptr(means3D), _ptr(sh), _ptr(colors), _ptr(segments)
+    i.opacities, i.scales, i.rotations, i.cov3D_precomp = _ptr(opacity), _ptr(scales), _ptr(rotations), _ptr(
+        cov3D_precomp)
+    return i
+
+
+def _check_segments(segments, P):
+    if segments is not None and (segments.dim() != 2 or segments.shape[1] != NUM_CLASS or segments.shape[0] != P):
+        raise RuntimeError(f"segments must have shape (num_points, {NUM_CLASS}) (reference config.h:16 NUM_CLASS)")
+
+
+def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, rotations, scale_modifier,
+                        cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh,
+                        degree, campos, prefiltered, debug):
+    """RasterizeGaussiansCUDA (DGR/rasterize_points.cu:35-125).
+    Returns (num_rendered, color, depth, segment, alpha, radii, geomBuffer, binningBuffer, imgBuffer)."""
+    if means3D.dim() != 2 or means3D.size(1) != 3:
+        raise RuntimeError("means3D must have dimensions (num_points, 3)")
+    P, H, W = int(means3D.size(0)), int(image_height), int(image_width)
+    device = means3D.device
+    if device.type != "cuda":
+        raise RuntimeError("gsr rasterizer: means3D must be a GPU tensor (the HIP path has no CPU fallback)")
+    with torch.cuda.device(device):
+        f32 = dict(dtype=torch.float32, device=device)
+        if P == 0:  # reference leaves the zero-filled outputs untouched (rasterize_points.cu:87)
+            z = lambda *s: torch.zeros(*s, **f32)
+            empty = torch.empty(0, dtype=torch.uint8, device=device)
+            return (0, z(NUM_CHANNELS, H, W), z(1, H, W), z(NUM_CLASS, H, W), z(1, H, W),
+                    torch.zeros(0, dtype=torch.int32, device=device), empty, empty.clone(), empty.clone())
+        means3D_ = _dev_f32(means3D, device, "means3D")
+        sh_ = _dev_f32(sh, device, "sh")
+        colors_ = _dev_f32(colors, device, "colors_precomp")
+        segments_ = _dev_f32(segments, device, "segments", align=8)
+        _check_segments(segments_, P)
+        opacity_ = _dev_f32(opacity, device, "opacities")
+        scales_ = _dev_f32(scales, device, "scales")
+        rotations_ = _dev_f32(rotations, device, "rotations", align=16)
+        cov_ = _dev_f32(cov3D_precomp, device, "cov3D_precomp")
+        bg_ = _dev_f32(background, device, "bg")
+        view_ = _dev_f32(viewmatrix, device, "viewmatrix")
+        proj_ = _dev_f32(projmatrix, device, "projmatrix")
+        campos_ = _dev_f32(campos, device, "campos")
+        M = int(sh_.size(1)) if sh_ is not None else 0
+        s = _settings(P, int(degree), M, W, H, tan_fovx, tan_fovy, scale_modifier, prefiltered, debug, bg_, view_,
+                      proj_, campos_)
+        inp = _inputs(means3D_, sh_, colors_, segments_, opacity_, scales_, rotations_, cov_)
+        stream = _stream(device)
+        u8 = dict(dtype=torch.uint8, device=device)
+        geom = torch.empty(_lib.gsr_geom_bytes(P), **u8)
+        img = torch.empty(_lib.gsr_img_bytes(W, H), **u8)
+        radii = torch.empty(P, dtype=torch.int32, device=device)
+        nr = ctypes.c_int(0)
+        _check(_lib.gsr_forward_geometry(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), radii.data_ptr(),
+                                         stream, ctypes.byref(nr)))
+        num_rendered = int(nr.value)
+        binning = torch.empty(_lib.gsr_binning_bytes(num_rendered), **u8)
+        color = torch.empty(NUM_CHANNELS, H, W, **f32)
+        depth = torch.empty(1, H, W, **f32)
+        alpha = torch.empty(1, H, W, **f32)
+        segment = torch.empty(NUM_CLASS, H, W, **f32)
+        _check(_lib.gsr_forward_render(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), binning.data_ptr(),
+                                       img.data_ptr(), num_rendered, color.data_ptr(), depth.data_ptr(),
+                                       alpha.data_ptr(), segment.data_ptr(), stream))
+    return num_rendered, color, depth, segment, alpha, radii, geom, binning, img
+
+
+def grad_arena_layout(P, M):
+    """Offsets (in floats) of the gradients inside the single arena allocated by
+    rasterize_gaussians_backward.  The first `bucket` floats are the parameter
+    gradients a data-parallel trainer all-reduces: [dmeans3D | dsh | dopacity |
+    dscales | drot | dsegments]; means2D/colour/cov3D grads follow."""
+    sizes = [("dmeans3D", 3), ("dsh", 3 * M), ("dopacity", 1), ("dscales", 3), ("drot", 4),
+             ("dsegments", NUM_CLASS), ("dmeans2D", 3), ("dcolors", 3), ("dcov3D", 6)]
+    off, o = {}, 0
+    for n, k in sizes:
+        off[n] = (o, k)
+        o += k * P
+        if n == "dsegments":
+            off["bucket"] = (0, o)
+    off["total"] = (0, o)
+    return off
+
+
+def rasterize_gaussians_backward(background, means3D, radii, colors, segments, scales, rotations, scale_modifier,
+                                 cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
+                                 dL_dout_segment, dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer, R,
+                                 binningBuffer, imageBuffer, alpha, debug):
+    """RasterizeGaussiansBackwardCUDA (DGR/rasterize_points.cu:127-221).
+    Returns (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
+    dL_drotations, dL_dsegments); gradients of absent (empty) inputs are None."""
+    P = int(means3D.size(0))
+    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    device = means3D.device
+    with torch.cuda.device(device):
+        means3D_ = _dev_f32(means3D, device, "means3D")
+        sh_ = _dev_f32(sh, device, "sh")
+        colors_ = _dev_f32(colors, device, "colors_precomp")
+        segments_ = _dev_f32(segments, device, "segments", align=8)
+        scales_ = _dev_f32(scales, device, "scales")
+        rotations_ = _dev_f32(rotations, device, "rotations", align=16)
+        cov_ = _dev_f32(cov3D_precomp, device, "cov3D_precomp")
+        M = int(sh_.size(1)) if sh_ is not None else 0
+        lay = grad_arena_layout(P, M)
+        arena = torch.empty(lay["total"][1], dtype=torch.float32, device=device)
+
+        def view(name, *shape):
+            o, k = lay[name]
+            return arena.narrow(0, o, k * P).view(P, *shape)
+
+        dmeans3D, dsh, dopacity = view("dmeans3D", 3), view("dsh", M, 3), view("dopacity", 1)
+        dscales, drot, dsegments = view("dscales", 3), view("drot", 4), view("dsegments", NUM_CLASS)
+        dmeans2D, dcolors, dcov3D = view("dmeans2D", 3), view("dcolors", 3), view("dcov3D", 6)
+        if P == 0:
+            arena.zero_()
+            return dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot, dsegments
+        bg_ = _dev_f32(background, device, "bg")
+        view_ = _dev_f32(viewmatrix, device, "viewmatrix")
+        proj_ = _dev_f32(projmatrix, device, "projmatrix")
+        campos_ = _dev_f32(campos, device, "campos")
+        s = _settings(P, int(degree), M, W, H, tan_fovx, tan_fovy, scale_modifier, False, debug, bg_, view_, proj_,
+                      campos_)
+        inp = _inputs(means3D_, sh_, colors_, segments_, None, scales_, rotations_, cov_)  # opacities unused
+        ups = [_dev_f32(t, device, n) for t, n in ((dL_dout_color, "dL_dcolor"), (dL_dout_segment, "dL_dsegment"),
+                                                   (dL_dout_depth, "dL_ddepth"), (dL_dout_alpha, "dL_dalpha"))]
+        ups = [u if u is not None else torch.zeros(1, H, W, dtype=torch.float32, device=device) for u in ups]
+        alpha_ = _dev_f32(alpha, device, "alpha")
+        radii_ = radii.contiguous()
+        R = int(R)
+        scratch = torch.empty(_lib.gsr_backward_scratch_bytes(R), dtype=torch.uint8, device=device)
+        g = _Grads()
+        g.dmeans2D, g.dopacity, g.dmeans3D = dmeans2D.data_ptr(), dopacity.data_ptr(), dmeans3D.data_ptr()
+        g.dcolors = dcolors.data_ptr() if colors_ is not None else None
+        g.dcov3D = dcov3D.data_ptr() if cov_ is not None else None
+        g.dsh = dsh.data_ptr() if (sh_ is not None and M > 0) else None
+        g.dscales = dscales.data_ptr() if scales_ is not None else None
+        g.drot = drot.data_ptr() if scales_ is not None else None
+        g.dsegments = dsegments.data_ptr()
+        _check(_lib.gsr_backward(ctypes.byref(s), ctypes.byref(inp), radii_.data_ptr(), geomBuffer.data_ptr(),
+                                 binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
+                                 R, alpha_.data_ptr(), ups[0].data_ptr(), ups[1].data_ptr(), ups[2].data_ptr(),
+                                 ups[3].data_ptr(), scratch.data_ptr() if R > 0 else None, ctypes.byref(g),
+                                 _stream(device)))
+    return (dmeans2D, dcolors if colors_ is not None else None, dopacity, dmeans3D,
+            dcov3D if cov_ is not None else None, dsh if sh_ is not None else None,
+            dscales if scales_ is not None else None, drot if scales_ is not None else None,
+            dsegments if segments_ is not None else None)
+
+
+def mark_visible(means3D, viewmatrix, projmatrix):
+    """markVisible (DGR/rasterize_points.cu:223-242): bool [P]."""
+    P = int(means3D.size(0))
+    device = means3D.device
+    with torch.cuda.device(device):
+        present = torch.zeros(P, dtype=torch.bool, device=device)
+        if P == 0:
+            return present
+        m = _dev_f32(means3D, device, "means3D")
+        v = _dev_f32(viewmatrix, device, "viewmatrix")
+        p = _dev_f32(projmatrix, device, "projmatrix")
+        _check(_lib.gsr_mark_visible(P, m.data_ptr(), v.data_ptr(), p.data_ptr(), present.data_ptr(),
+                                     _stream(device)))
+    return present

@@ -1,0 +1,157 @@
+/*
+ * gsr.h -- C ABI of the MI355X-native differentiable Gaussian rasterizer
+ * (libgsr.so, built from 3d_gaussian_magic_change-segment_3dgs_amd/csrc/).
+ *
+ * Drop-in boundary for the reference's private extension module
+ * `diff_gaussian_rasterization._C` (DGR/ext.cpp:15-19).  The Python package
+ * diff_gaussian_rasterization (same directory tree) binds these symbols with
+ * ctypes and keeps the reference's public API (GaussianRasterizationSettings,
+ * GaussianRasterizer, rasterize_gaussians: DGR/diff_gaussian_rasterization/
+ * __init__.py:21-236) unchanged.
+ *
+ * Conventions
+ *   - Plain C: no C++ or HIP types.  `stream` is a hipStream_t passed as void*
+ *     (torch.cuda.current_stream().cuda_stream); NULL = legacy default stream.
+ *   - Every array pointer is a device pointer owned by the caller; the library
+ *     never allocates device memory.  A NULL input pointer means "absent",
+ *     mirroring the reference's empty-tensor convention (DGR/diff_gaussian_
+ *     rasterization/__init__.py:208-221): exactly one of shs / colors_precomp,
+ *     exactly one of (scales+rotations) / cov3D_precomp.  segments == NULL is
+ *     read as zeros (the reference dereferences it unconditionally,
+ *     forward.cu:369).
+ *   - fp32 everywhere; images are planar CHW like the reference outputs
+ *     (forward.cu:383-391).
+ *   - Return value: 0 = success; non-zero = error, message in gsr_last_error()
+ *     (thread-local).  settings->debug != 0 synchronises the stream after each
+ *     stage and reports the first failing stage (reference CHECK_CUDA,
+ *     auxiliary.h:166-173).
+ *   - No global mutable device state: concurrent calls on distinct buffers and
+ *     streams are safe (one process per GPU under torchrun).
+ */
+#ifndef GSR_H_
+#define GSR_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#if defined(__GNUC__) || defined(__clang__)
+#define GSR_API __attribute__((visibility("default")))
+#else
+#define GSR_API
+#endif
+
+#define GSR_NUM_CHANNELS 3 /* reference config.h:15 */
+#define GSR_NUM_CLASS 2    /* reference config.h:16 */
+#define GSR_BLOCK_X 16     /* reference config.h:17 */
+#define GSR_BLOCK_Y 16     /* reference config.h:18 */
+
+/* Raster settings: the fields of GaussianRasterizationSettings
+ * (DGR/diff_gaussian_rasterization/__init__.py:168-180) plus the problem sizes
+ * the reference derives in RasterizeGaussiansCUDA (rasterize_points.cu:62-93). */
+typedef struct gsr_settings {
+    int P;                 /* number of Gaussians (means3D.shape[0]) */
+    int D;                 /* active SH degree (sh_degree), 0..3 */
+    int M;                 /* SH coefficients per channel (shs.shape[1]); 0 if shs absent */
+    int W, H;              /* image_width, image_height */
+    float tanfovx, tanfovy;
+    float scale_modifier;
+    int prefiltered;       /* accepted for API parity; culled points are never an error here */
+    int debug;
+    const float* bg;         /* device [3] */
+    const float* viewmatrix; /* device [16], W2C^T row-major (scene/cameras.py:58) */
+    const float* projmatrix; /* device [16], viewmatrix @ proj^T (scene/cameras.py:60) */
+    const float* campos;     /* device [3] */
+} gsr_settings;
+
+/* Per-Gaussian inputs (device pointers, NULL = absent). */
+typedef struct gsr_inputs {
+    const float* means3D;        /* [P,3] */
+    const float* shs;            /* [P,M,3] */
+    const float* colors_precomp; /* [P,3] */
+    const float* segments;       /* [P,2] */
+    const float* opacities;      /* [P,1] (activated) */
+    const float* scales;         /* [P,3] (activated) */
+    const float* rotations;      /* [P,4] wxyz, normalised by the caller */
+    const float* cov3D_precomp;  /* [P,6] upper triangle */
+} gsr_inputs;
+
+/* Gradient outputs of gsr_backward (device pointers; NULL = not wanted).
+ * Every element of a non-NULL array is written (no pre-zeroing needed).
+ * Replaces the zero-initialised tensors of rasterize_points.cu:166-177. */
+typedef struct gsr_grads {
+    float* dmeans2D;   /* [P,3]  NDC-space screen gradient, z = 0 */
+    float* dcolors;    /* [P,3]  (grad of colors_precomp) */
+    float* dopacity;   /* [P,1] */
+    float* dmeans3D;   /* [P,3] */
+    float* dcov3D;     /* [P,6]  (grad of cov3D_precomp) */
+    float* dsh;        /* [P,M,3]; coefficients >= (D+1)^2 are written as 0 */
+    float* dscales;    /* [P,3] */
+    float* drot;       /* [P,4] */
+    float* dsegments;  /* [P,2] */
+} gsr_grads;
+
+/* ---- size queries: the three byte buffers of the reference
+ * (GeometryState / BinningState / ImageState, rasterizer_impl.h:29-73).  The
+ * layout is private to the library and identical between forward and backward
+ * for the same arguments. */
+GSR_API size_t gsr_geom_bytes(int P);
+GSR_API size_t gsr_binning_bytes(int num_rendered);
+GSR_API size_t gsr_img_bytes(int W, int H);
+/* scratch needed by gsr_backward (per-instance gradient records) */
+GSR_API size_t gsr_backward_scratch_bytes(int num_rendered);
+
+/* ---- forward, stage A: preprocess (projection, covariance, SH), depth order,
+ * per-Gaussian tile counts and their prefix sum; copies num_rendered to the
+ * host (the reference's single host sync, rasterizer_impl.cu:284-285).
+ * Replaces Rasterizer::forward lines :226-289.  radii: device int32 [P]. */
+GSR_API int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii,
+                         void* stream, int* num_rendered);
+
+/* ---- forward, stage B: key duplication, tile sort, tile ranges and the tile
+ * blend.  Replaces Rasterizer::forward lines :291-343 (duplicateWithKeys,
+ * SortPairs, identifyTileRanges, renderCUDA).  Outputs: out_color [3,H,W],
+ * out_depth [1,H,W], out_alpha [1,H,W] (= sum of alpha*T, forward.cu:386),
+ * out_segment [2,H,W]. */
+GSR_API int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, void* binning,
+                       void* img, int num_rendered, float* out_color, float* out_depth,
+                       float* out_alpha, float* out_segment, void* stream);
+
+/* ---- backward.  Replaces Rasterizer::backward (rasterizer_impl.cu:348-458) /
+ * RasterizeGaussiansBackwardCUDA (rasterize_points.cu:127-221).  dL_d* are the
+ * upstream image gradients (same shapes as the forward outputs); alpha is the
+ * forward's out_alpha; scratch has gsr_backward_scratch_bytes(num_rendered). */
+GSR_API int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, void* geom,
+                 void* binning, void* img, int num_rendered, const float* alpha,
+                 const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
+                 const float* dL_dalpha, void* scratch, const gsr_grads* grads, void* stream);
+
+/* ---- frustum visibility: present[i] = (view-space z > 0.2).  Replaces
+ * markVisible (rasterize_points.cu:223-242, rasterizer_impl.cu:54-66). */
+GSR_API int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,
+                     uint8_t* present, void* stream);
+
+/* ---- inspection hook for parity tests: copies one private intermediate of a
+ * forward call into dst (device memory; stream-ordered).  Names and element
+ * types: "tiles_touched" u32[P], "rec" f32[P,16] ({x,y,conic.xyz,opacity,depth,
+ * seg0,r,g,b,seg1,0...}), "clamped" u8[P], "order" u32[P] (depth order),
+ * "goff" u32[P], "point_list" u32[I], "slot_vals" u32[I], "ranges" u32[T,2],
+ * "n_contrib_tiles" u32[T,256] (tile-major, entry k*64+l = pixel
+ * (16*tx + (l&15), 16*ty + (l>>4) + 4k)).  Returns the byte count copied, or -1. */
+GSR_API long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered, void* geom,
+                                 void* binning, void* img, void* dst, void* stream);
+
+/* Thread-local message of the last failing call ("" if none). */
+GSR_API const char* gsr_last_error(void);
+
+/* Library version string (build identification). */
+GSR_API const char* gsr_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GSR_H_ */
