@@ -2,12 +2,67 @@
 // Reference orchestration: DGR/cuda_rasterizer/rasterizer_impl.cu:198-458 and
 // the host bindings DGR/rasterize_points.cu:35-242.
 #include <stdio.h>
+#include <mutex>
 #include <string>
+#include <vector>
 
 #include "gsr_internal.h"
 
 namespace {
 thread_local std::string g_last_error;
+
+// ---- live stage timing (gsr_timing_*): hipEvents on the caller's stream.
+constexpr int NUM_STAGES = 9;
+const char* const STAGE_NAMES[NUM_STAGES] = {"preprocess", "depth_sort", "scan",       "duplicate",   "tile_sort",
+                                             "ranges",     "render_fwd", "render_bwd", "gaussian_bwd"};
+struct Timer {
+    std::mutex mu;
+    bool on = false;
+    struct Rec { int stage; hipEvent_t a, b; };
+    std::vector<Rec> pending;
+    std::vector<hipEvent_t> pool;
+    hipEvent_t get() {
+        if (!pool.empty()) {
+            hipEvent_t e = pool.back();
+            pool.pop_back();
+            return e;
+        }
+        hipEvent_t e = nullptr;
+        if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+        return e;
+    }
+};
+Timer& timer() {
+    static Timer t;
+    return t;
+}
+struct StageScope {
+    int stage;
+    hipStream_t st;
+    hipEvent_t a = nullptr;
+    StageScope(int s, hipStream_t stream) : stage(s), st(stream) {
+        Timer& T = timer();
+        std::lock_guard<std::mutex> lk(T.mu);
+        if (!T.on) return;
+        a = T.get();
+        if (a && hipEventRecord(a, st) != hipSuccess) {
+            T.pool.push_back(a);
+            a = nullptr;
+        }
+    }
+    ~StageScope() {
+        if (!a) return;
+        Timer& T = timer();
+        std::lock_guard<std::mutex> lk(T.mu);
+        hipEvent_t b = T.get();
+        if (!b || hipEventRecord(b, st) != hipSuccess) {
+            T.pool.push_back(a);
+            if (b) T.pool.push_back(b);
+            return;
+        }
+        T.pending.push_back({stage, a, b});
+    }
+};
 
 int fail(const std::string& msg) {
     g_last_error = msg;
@@ -84,16 +139,25 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
     const ImgLayout IL = img_layout(s->W, s->H);
     const GeomLayout L = geom_layout(P);
     char* g = aligned_base(geom);
-    launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
-                      at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect), st);
+    {
+        StageScope sc(GSR_STAGE_PREPROCESS, st);
+        launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
+                          at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect), st);
+    }
     GSR_STAGE("preprocess");
-    // Depth order: 32-bit keys -> 4 passes (even: sorted keys land back in depth_keys).
-    launch_radix_sort(at<uint32_t>(g, L.depth_keys), nullptr, at<uint32_t>(g, L.dkeys_alt),
-                      at<uint32_t>(g, L.order_alt), at<uint32_t>(g, L.depth_keys), at<uint32_t>(g, L.order), P, 32,
-                      at<uint32_t>(g, L.hist), at<uint32_t>(g, L.parts), st);
+    {
+        // Depth order: 32-bit keys -> 4 passes (even: sorted keys land back in depth_keys).
+        StageScope sc(GSR_STAGE_DEPTH_SORT, st);
+        launch_radix_sort(at<uint32_t>(g, L.depth_keys), nullptr, at<uint32_t>(g, L.dkeys_alt),
+                          at<uint32_t>(g, L.order_alt), at<uint32_t>(g, L.depth_keys), at<uint32_t>(g, L.order), P,
+                          32, at<uint32_t>(g, L.hist), at<uint32_t>(g, L.parts), st);
+    }
     GSR_STAGE("depth sort");
-    launch_scan_inclusive_gather(at<uint32_t>(g, L.tiles_touched), at<uint32_t>(g, L.order),
-                                 at<uint32_t>(g, L.offsets), P, at<uint32_t>(g, L.parts), st);
+    {
+        StageScope sc(GSR_STAGE_SCAN, st);
+        launch_scan_inclusive_gather(at<uint32_t>(g, L.tiles_touched), at<uint32_t>(g, L.order),
+                                     at<uint32_t>(g, L.offsets), P, at<uint32_t>(g, L.parts), st);
+    }
     GSR_STAGE("scan");
     uint32_t total = 0;
     hipError_t e = hipMemcpyAsync(&total, at<uint32_t>(g, L.offsets) + (P - 1), sizeof(uint32_t),
@@ -128,9 +192,12 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
     uint32_t* point_list = nullptr;
     if (I > 0) {
         if (!geom || !binning) return fail("[gsr] geom/binning buffers are NULL");
-        launch_duplicate(P, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets), at<uint32_t>(g, GL.tiles_touched),
-                         at<ushort4>(g, GL.rect), IL.gx, at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid),
-                         at<uint32_t>(g, GL.goff), st);
+        {
+            StageScope sc(GSR_STAGE_DUPLICATE, st);
+            launch_duplicate(P, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets),
+                             at<uint32_t>(g, GL.tiles_touched), at<ushort4>(g, GL.rect), IL.gx,
+                             at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid), at<uint32_t>(g, GL.goff), st);
+        }
         GSR_STAGE("duplicate");
         const int bits = (int)higher_msb((uint32_t)T);
         const int passes = (bits + RADIX_BITS - 1) / RADIX_BITS;
@@ -139,15 +206,25 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
         uint32_t* kalt = at<uint32_t>(b, BL.tkeys_alt);
         uint32_t* kout = (passes % 2 == 0) ? kin : kalt;
         uint32_t* ktmp = (passes % 2 == 0) ? kalt : kin;
-        launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout, at<uint32_t>(b, BL.slot_vals), I,
-                          bits, at<uint32_t>(b, BL.hist), at<uint32_t>(b, BL.parts), st);
+        {
+            StageScope sc(GSR_STAGE_TILE_SORT, st);
+            launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout, at<uint32_t>(b, BL.slot_vals),
+                              I, bits, at<uint32_t>(b, BL.hist), at<uint32_t>(b, BL.parts), st);
+        }
         GSR_STAGE("tile sort");
         point_list = at<uint32_t>(b, BL.point_list);
-        launch_finalize(I, kout, at<uint32_t>(b, BL.slot_vals), at<uint32_t>(b, BL.slot_gid), point_list, ranges, st);
+        {
+            StageScope sc(GSR_STAGE_RANGES, st);
+            launch_finalize(I, kout, at<uint32_t>(b, BL.slot_vals), at<uint32_t>(b, BL.slot_gid), point_list, ranges,
+                            st);
+        }
         GSR_STAGE("tile ranges");
     }
-    launch_render_forward(s->W, s->H, IL.gx, IL.gy, ranges, point_list, g ? at<float4>(g, GL.rec) : nullptr, s->bg,
-                          out_color, out_depth, out_alpha, out_segment, at<uint32_t>(im, IL.n_contrib), st);
+    {
+        StageScope sc(GSR_STAGE_RENDER_FWD, st);
+        launch_render_forward(s->W, s->H, IL.gx, IL.gy, ranges, point_list, g ? at<float4>(g, GL.rec) : nullptr,
+                              s->bg, out_color, out_depth, out_alpha, out_segment, at<uint32_t>(im, IL.n_contrib), st);
+    }
     GSR_STAGE("render");
     return 0;
 }
@@ -177,16 +254,48 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
         const BinLayout BL = bin_layout(I);
         char* b = aligned_base(binning);
         contrib = reinterpret_cast<float*>(aligned_base(scratch));
-        launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint2>(im, IL.ranges), at<uint32_t>(b, BL.point_list),
-                               at<uint32_t>(b, BL.slot_vals), at<float4>(g, GL.rec), s->bg, alpha,
-                               at<uint32_t>(im, IL.n_contrib), dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha,
-                               contrib, st);
+        {
+            StageScope sc(GSR_STAGE_RENDER_BWD, st);
+            launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint2>(im, IL.ranges),
+                                   at<uint32_t>(b, BL.point_list), at<uint32_t>(b, BL.slot_vals),
+                                   at<float4>(g, GL.rec), s->bg, alpha, at<uint32_t>(im, IL.n_contrib), dL_dcolor,
+                                   dL_dsegment, dL_ddepth, dL_dalpha, contrib, st);
+        }
         GSR_STAGE("render backward");
     }
-    launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
-                             at<uint8_t>(g, GL.clamped), contrib, *grads, st);
+    {
+        StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);
+        launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
+                                 at<uint8_t>(g, GL.clamped), contrib, *grads, st);
+    }
     GSR_STAGE("gaussian backward");
     return 0;
+}
+
+int gsr_num_stages(void) { return NUM_STAGES; }
+
+const char* gsr_stage_name(int stage) { return (stage >= 0 && stage < NUM_STAGES) ? STAGE_NAMES[stage] : ""; }
+
+void gsr_timing_enable(int on) {
+    Timer& T = timer();
+    std::lock_guard<std::mutex> lk(T.mu);
+    T.on = on != 0;
+}
+
+int gsr_timing_collect(double* ms, long long* counts) {
+    Timer& T = timer();
+    std::lock_guard<std::mutex> lk(T.mu);
+    for (auto& r : T.pending) {
+        float t = 0.f;
+        if (hipEventSynchronize(r.b) == hipSuccess && hipEventElapsedTime(&t, r.a, r.b) == hipSuccess) {
+            if (ms) ms[r.stage] += t;
+            if (counts) counts[r.stage] += 1;
+        }
+        T.pool.push_back(r.a);
+        T.pool.push_back(r.b);
+    }
+    T.pending.clear();
+    return NUM_STAGES;
 }
 
 long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered, void* geom, void* binning,

@@ -16,6 +16,21 @@
 // slots in fixed order: deterministic, atomic-free gradients.
 #include "gsr_internal.h"
 
+// Numerics.  The blend thresholds alpha >= 1/255 and T*(1-alpha) >= 1e-4
+// (forward.cu:352-359) make n_contrib and every contribution knife-edge
+// sensitive to exp(): the full-precision expf (ocml, ~1 ulp, like the
+// reference's CUDA expf) keeps threshold flips against the oracle to ~0 on the
+// parity scenes, where __expf (v_exp_f32 of x*log2e, several ulp at |x|~5)
+// flipped about one pair per 10^7.  GSR_FAST_EXP selects the fast form.
+// The forward blend keeps FMA contraction (errors ~2e-7); the backward replay
+// runs with contraction off so its long recurrences (T /= 1-alpha, accum_rec)
+// round like the reference's sequential code.
+#ifdef GSR_FAST_EXP
+#define GSR_EXP(x) __expf(x)
+#else
+#define GSR_EXP(x) expf(x)
+#endif
+
 namespace gsr {
 namespace {
 
@@ -78,7 +93,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
             for (int k = 0; k < 4; ++k) {
                 const float dx = gx_ - pfx, dy = gy_ - pfy[k];
                 const float power = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
-                alpha[k] = fminf(0.99f, op * __expf(power));
+                alpha[k] = fminf(0.99f, op * GSR_EXP(power));
                 bool o = !done[k] && power <= 0.0f && alpha[k] >= ALPHA_MIN;
                 const float test_T = T[k] * (1.f - alpha[k]);
                 const bool term = o && test_T < T_MIN;
@@ -171,6 +186,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
                                                    const float* __restrict__ dL_ddepths,
                                                    const float* __restrict__ dL_dalphas,
                                                    float* __restrict__ contrib) {
+#pragma clang fp contract(off)
     const int tile = blockIdx.x;
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
@@ -255,7 +271,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
                 dxs[k] = dx;
                 dys[k] = dy;
                 const float power = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
-                G[k] = __expf(power);
+                G[k] = GSR_EXP(power);
                 alpha[k] = fminf(0.99f, op * G[k]);
                 ok[k] = p < lastc[k] && power <= 0.0f && alpha[k] >= ALPHA_MIN;
                 any_ok = any_ok || ok[k];

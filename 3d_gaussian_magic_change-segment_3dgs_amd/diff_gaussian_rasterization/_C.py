@@ -70,9 +70,17 @@ _lib.gsr_version.restype = ctypes.c_char_p
 _lib.gsr_debug_copy.restype = ctypes.c_longlong
 _lib.gsr_debug_copy.argtypes = [ctypes.c_char_p, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]
 
+_lib.gsr_num_stages.restype = _i
+_lib.gsr_stage_name.restype = ctypes.c_char_p
+_lib.gsr_stage_name.argtypes = [_i]
+_lib.gsr_timing_enable.argtypes = [_i]
+_lib.gsr_timing_collect.restype = _i
+_lib.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
+
 EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_img_bytes", "gsr_backward_scratch_bytes",
                     "gsr_forward_geometry", "gsr_forward_render", "gsr_backward", "gsr_mark_visible",
-                    "gsr_debug_copy", "gsr_last_error", "gsr_version")
+                    "gsr_debug_copy", "gsr_num_stages", "gsr_stage_name", "gsr_timing_enable", "gsr_timing_collect",
+                    "gsr_last_error", "gsr_version")
 
 _DEBUG_FIELDS = {  # name -> (dtype, elements per unit, unit: P | I | T)
     "tiles_touched": (torch.int32, 1, "P"), "rec": (torch.float32, 16, "P"), "clamped": (torch.uint8, 1, "P"),

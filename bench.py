@@ -1,0 +1,234 @@
+#!/usr/bin/env python
+"""bench.py -- forward+backward views/s of the gsr rasterizer (BASELINE.json metric).
+
+One step = one view through the drop-in boundary: _RasterizeGaussians.forward
+(incl. the reference's num_rendered host sync) + .backward with fixed synthetic
+upstream gradients, on the synthetic metric scene (1M Gaussians,
+SH3, 2 segment classes, 1920x1080) resident in HBM.  With N GPUs (torchrun, one
+process per GPU) every rank renders its own view of the replicated scene and the
+parameter-gradient bucket (61 f32 / Gaussian) is summed with one RCCL all-reduce
+per step; value = N * steps / max-over-ranks elapsed (weak scaling in views).
+
+Prints ONE JSON line on rank 0.  Extra objects:
+  roofline     -- the dominant kernel (per-stage HIP events recorded by libgsr on
+                  the stream it launches on): algorithmic bytes per launch / mean
+                  launch time vs the 8 TB/s HBM peak; `traffic` = PMC-measured HBM
+                  bytes per launch from profiles/ when a counter profile exists.
+  cpu_baseline -- the CPU oracle (C++ restatement of the reference kernels,
+                  OpenMP) timed on this box's host cores on a bounded sample of the
+                  same workload (whole views, rank 0, N = 1 only).
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd")
+for p in (ROOT, PKG):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+import torch  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1_pmc_summary.json")
+
+
+def algorithmic_bytes(stage, P, I, HW, deg, launches_per_view=1):
+    """Bytes a stage must move per launch (DESIGN.md s4 lists the derivation)."""
+    ncoef = (deg + 1) ** 2
+    sh = 12 * ncoef
+    if stage == "preprocess":      # means,scales,rot,opac,seg,SH in; record,radii,tiles,key,clamp,rect out
+        return P * (12 + 12 + 16 + 4 + 8 + sh + 64 + 4 + 4 + 4 + 1 + 8)
+    if stage == "render_fwd":      # per instance: id + 48-B record; per pixel: 8 outputs + n_contrib
+        return I * (4 + 48) + HW * (12 + 4 + 4 + 8 + 4)
+    if stage == "render_bwd":      # per instance: id + slot + record in, 48-B gradient record out; per pixel ins
+        return I * (4 + 4 + 48 + 48) + HW * (4 + 4 + 12 + 8 + 4 + 4)
+    if stage == "gaussian_bwd":    # gradient records in + per-Gaussian params/SH in + all grads out
+        return I * 48 + P * (13 + 12 + 12 + 16 + sh + 12 + 4 + 12 + sh + 12 + 16 + 8)
+    if stage == "duplicate":       # order/offset/tiles/rect in; key + owner out per instance
+        return P * (4 + 4 + 4 + 8 + 4) + I * 8
+    if stage == "tile_sort":       # per pass: key+val in and out (first pass: no val in) + key re-read
+        return I * (4 + 8 + 8 + 8 + 4)
+    if stage == "ranges":
+        return I * (4 + 4 + 4 + 4 + 4)
+    if stage == "depth_sort":
+        return P * (4 + 8 + 3 * (8 + 8) + 8 + 4 * 4)
+    if stage == "scan":
+        return P * (4 + 4 + 4 + 4)
+    return 0
+
+
+def view_bytes(P, I, HW, deg):
+    """SURVEY.md s8d whole-view algorithmic bytes: (446 + 36 M) P + 148 I + 68 HW."""
+    M = (deg + 1) ** 2
+    return (446 + 36 * M) * P + 148 * I + 68 * HW
+
+
+def cpu_baseline(scene, cam, grads, budget_s=20.0):
+    from oracle import oracle as O
+    O.build()
+    up = [grads[k].numpy() for k in ("color", "segment", "depth", "alpha")]
+    t0 = time.perf_counter()
+    r = O.run_scene(scene, cam)
+    r.backward(*up)
+    one = time.perf_counter() - t0
+    reps = int(max(1, min(10, budget_s // max(one, 1e-3))))
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        r = O.run_scene(scene, cam)
+        r.backward(*up)
+    el = time.perf_counter() - t0
+    return {"value": reps / el, "unit": "views/s", "cores": int(O.lib().oracle_num_threads()), "kind": "port",
+            "sample": f"{reps} whole fwd+bwd views of the benchmark workload (P={scene.P}, "
+                      f"{cam.width}x{cam.height}, SH{scene.sh_degree}) after 1 warm-up view; "
+                      f"oracle/gsr_oracle.cpp built -O3 -fopenmp"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--config", default="mt", help="gsr_tools.scene.CONFIGS key (default: the metric config)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work for cpu_baseline")
+    ap.add_argument("--stages", action="store_true", help="print the per-stage table to stderr")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        if world == 1 and args.gpus > 1:
+            sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=device)
+
+    from gsr_tools.scene import config_scene_and_camera, CONFIGS
+    import diff_gaussian_rasterization as dgr
+    from diff_gaussian_rasterization import _C
+
+    scene_cpu, cam_cpu = config_scene_and_camera(args.config, view_index=rank, n_views=max(8, world))
+    P, W, H, deg = scene_cpu.P, cam_cpu.width, cam_cpu.height, scene_cpu.sh_degree
+    gen = torch.Generator().manual_seed(1)
+    ups_cpu = {k: (torch.randn(c, H, W, generator=gen) * 1e-3) for k, c in
+               (("color", 3), ("depth", 1), ("alpha", 1), ("segment", 2))}
+    ups = {k: v.to(device) for k, v in ups_cpu.items()}
+    leaf = lambda t: t.to(device).contiguous().requires_grad_(True)
+    means3D, shs, opac = leaf(scene_cpu.means3D), leaf(scene_cpu.shs), leaf(scene_cpu.opacities)
+    scales, rots, segs = leaf(scene_cpu.scales), leaf(scene_cpu.rotations), leaf(scene_cpu.segments)
+    means2D = torch.zeros_like(means3D, requires_grad=True)
+    E = torch.empty(0, device=device)
+    settings = dgr.GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=cam_cpu.tanfovx, tanfovy=cam_cpu.tanfovy,
+        bg=torch.zeros(3, device=device), scale_modifier=1.0, viewmatrix=cam_cpu.world_view_transform.to(device),
+        projmatrix=cam_cpu.full_proj_transform.to(device), sh_degree=deg, campos=cam_cpu.camera_center.to(device),
+        prefiltered=False, debug=False)
+    inputs = [means3D, means2D, shs, opac, scales, rots, segs]
+    lay = _C.grad_arena_layout(P, shs.shape[1])
+    state = {"I": 0}
+
+    def step():
+        color, radii, depth, alpha, segment = dgr.rasterize_gaussians(means3D, means2D, shs, E, segs, opac, scales,
+                                                                      rots, E, settings)
+        state["I"] = color.grad_fn.num_rendered
+        g = torch.autograd.grad([color, depth, alpha, segment],
+                                inputs, [ups["color"], ups["depth"], ups["alpha"], ups["segment"]])
+        if dist is not None:
+            arena = g[0]._base
+            assert arena is not None and arena.data_ptr() == g[0].data_ptr()
+            dist.all_reduce(arena.narrow(0, 0, lay["bucket"][1]))
+        return g
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    nst = _C._lib.gsr_num_stages()
+    import ctypes
+    ms = (ctypes.c_double * nst)()
+    cnt = (ctypes.c_longlong * nst)()
+    _C._lib.gsr_timing_collect(ms, cnt)  # drop warm-up events (timing off: no-op)
+    ms = (ctypes.c_double * nst)()
+    cnt = (ctypes.c_longlong * nst)()
+    _C._lib.gsr_timing_enable(1)
+    if dist is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    if dist is not None:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    _C._lib.gsr_timing_enable(0)
+    _C._lib.gsr_timing_collect(ms, cnt)
+    if dist is not None:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    I, HW = int(state["I"]), W * H
+    stages = {}
+    for i in range(nst):
+        name = _C._lib.gsr_stage_name(i).decode()
+        if cnt[i]:
+            avg = ms[i] / cnt[i]
+            launches_per_step = cnt[i] / args.steps
+            stages[name] = {"avg_ms": round(avg, 4), "ms_per_step": round(ms[i] / args.steps, 4),
+                            "launches_per_step": launches_per_step,
+                            "gbs": round(algorithmic_bytes(name, P, I, HW, deg) / (avg * 1e-3) / 1e9, 1)}
+    dom = max(stages, key=lambda k: stages[k]["ms_per_step"]) if stages else None
+    value = world * args.steps / elapsed
+    roof = None
+    if dom:
+        achieved = stages[dom]["gbs"]
+        traffic = None
+        if os.path.exists(PMC_SUMMARY):
+            try:
+                pm = json.load(open(PMC_SUMMARY))
+                traffic = pm.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg),
+                "avg_launch_ms": stages[dom]["avg_ms"],
+                "whole_view_frac": round(view_bytes(P, I, HW, deg) * value / world / 1e9 / HBM_PEAK_GBS, 4)}
+    out = {
+        "metric": "forward+backward views/sec @1080p, 1M Gaussians, 1/2/4/8 MI355X",
+        "value": round(value, 2), "unit": "views/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f32", "data": "synthetic (SURVEY.md s8d generator, seed 0; upstream grads "
+                                                    "N(0,1)*1e-3 seed 1)",
+        "config": {"workload": f"{args.config}: P={P} Gaussians, SH{deg}, {W}x{H}, fwd+bwd per view at the "
+                               f"GaussianRasterizer boundary", "P": P, "width": W, "height": H, "sh_degree": deg,
+                   "num_classes": 2, "num_rendered": I, "global_batch": world, "views_per_step_per_gpu": 1,
+                   "parallelism": f"dp{world}" + (" (views sharded; RCCL all-reduce of the 61 f32/Gaussian "
+                                                  "grad bucket per step)" if world > 1 else "")},
+        "roofline": roof,
+        "stages": stages,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(scene_cpu, cam_cpu, ups_cpu, args.cpu_budget)
+    else:
+        out["cpu_baseline"] = None
+    if rank == 0:
+        if args.stages:
+            for k, v in stages.items():
+                print(f"{k:14s} {v['ms_per_step']:8.4f} ms/step  {v['gbs']:8.1f} GB/s", file=sys.stderr)
+        print(json.dumps(out), flush=True)
+    if dist is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

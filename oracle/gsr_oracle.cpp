@@ -505,7 +505,9 @@ int oracle_backward(void* h, const OracleInputs* in, const float* dL_dpix, const
     const float focal_x = W / (2.0f * s.tanfovx);
     const float* colors = in->colors_precomp ? in->colors_precomp : st->rgb.data();
     const float* segs = st->segments.data();
-    std::vector<float> contrib((size_t)I * 12, 0.f);
+    // fp64 accumulation: the reference sums with atomicAdd in arbitrary order, so
+    // the exact sum of the fp32 per-pixel terms is the centre of its outputs.
+    std::vector<double> contrib((size_t)I * 12, 0.0);
     const float ddelx_dx = 0.5 * W, ddely_dy = 0.5 * H;
 
     // renderCUDA backward (backward.cu:414-639)
@@ -545,7 +547,7 @@ int oracle_backward(void* h, const OracleInputs* in, const float* dL_dpix, const
                     if (alpha < 1.0f / 255.0f) continue;
                     Tr = Tr / (1.f - alpha);
                     const float dchannel_dcolor = alpha * Tr;
-                    float* cb = &contrib[(size_t)k * 12];
+                    double* cb = &contrib[(size_t)k * 12];
                     float dL_dopa = 0.0f;
                     for (int ch = 0; ch < NCH; ++ch) {
                         const float c = colors[g * NCH + ch];
@@ -587,11 +589,12 @@ int oracle_backward(void* h, const OracleInputs* in, const float* dL_dpix, const
             }
     }
     // Gather per-gaussian sums: [dcolor3 dseg2 ddepth dmean2D.xy dconic.xyw dopacity]
-    std::vector<float> gsum((size_t)P * 12, 0.f);
+    std::vector<double> gsum_d((size_t)P * 12, 0.0);
     for (int k = 0; k < I; ++k) {
         const uint32_t g = st->point_list[k];
-        for (int j = 0; j < 12; ++j) gsum[(size_t)g * 12 + j] += contrib[(size_t)k * 12 + j];
+        for (int j = 0; j < 12; ++j) gsum_d[(size_t)g * 12 + j] += contrib[(size_t)k * 12 + j];
     }
+    std::vector<float> gsum(gsum_d.begin(), gsum_d.end());
     std::vector<float> ddepth(P);
     for (int g = 0; g < P; ++g) {
         const float* q = &gsum[(size_t)g * 12];

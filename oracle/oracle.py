@@ -150,7 +150,7 @@ def settings_from_camera(cam, P, sh_degree, M, bg=(0.0, 0.0, 0.0), scale_modifie
 
 
 def run_scene(scene, cam, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=None, cov3D_precomp=None,
-              segments="scene"):
+              segments="scene", sh_degree=None):
     """Forward over a gsr_tools.scene.Scene with the reference's default argument path
     (shs + scales/rotations) unless precomputed colours / covariances are given."""
     inputs = {"means3D": _f32(scene.means3D), "opacities": _f32(scene.opacities)}
@@ -166,7 +166,8 @@ def run_scene(scene, cam, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp
     else:
         inputs["cov3D_precomp"] = _f32(cov3D_precomp)
     inputs["segments"] = _f32(scene.segments) if isinstance(segments, str) else _f32(segments)
-    st = settings_from_camera(cam, scene.P, scene.sh_degree, M, bg=bg, scale_modifier=scale_modifier)
+    D = scene.sh_degree if sh_degree is None else sh_degree
+    st = settings_from_camera(cam, scene.P, D, M, bg=bg, scale_modifier=scale_modifier)
     return OracleRun(st, inputs)
 
 

@@ -91,10 +91,10 @@ def untile_n_contrib(tiles, W, H):
 
 
 def run_oracle(oracle_mod, scene, cam, bg=(0.0, 0.0, 0.0), scale_modifier=1.0, colors_precomp=None,
-               cov3D_precomp=None, use_segments=True, grads=None):
+               cov3D_precomp=None, use_segments=True, grads=None, sh_degree=None):
     run = oracle_mod.run_scene(scene, cam, bg=bg, scale_modifier=scale_modifier, colors_precomp=colors_precomp,
                                cov3D_precomp=cov3D_precomp,
-                               segments="scene" if use_segments else None)
+                               segments="scene" if use_segments else None, sh_degree=sh_degree)
     res = {"color": run.color, "depth": run.depth, "alpha": run.alpha, "segment": run.segment,
            "radii": run.radii, "num_rendered": run.num_rendered}
     for k in ("tiles_touched", "point_list", "ranges", "n_contrib", "means2D", "conic_opacity", "depths", "rgb",

@@ -1,0 +1,112 @@
+"""The drop-in API on the GPU, called exactly the way the reference's
+gaussian_renderer/__init__.py:314-373 calls it."""
+import os
+
+import numpy as np
+import pytest
+import torch
+
+import harness as Hn
+from gsr_tools.scene import synthetic_scene, orbit_camera
+
+pytestmark = pytest.mark.gpu
+
+
+def _renderer_style_call(scene, cam, debug=False):
+    """Mirror of render() in gaussian_renderer/__init__.py (activations on parameters,
+    screenspace_points with retain_grad, kwargs call, 5 outputs, depth/max)."""
+    from diff_gaussian_rasterization import GaussianRasterizationSettings, GaussianRasterizer
+    dev = "cuda"
+    xyz = torch.nn.Parameter(scene.means3D.to(dev))
+    opacity_raw = torch.nn.Parameter(torch.logit(scene.opacities.to(dev)))
+    seg_raw = torch.nn.Parameter(torch.logit(scene.segments.to(dev)))
+    scale_raw = torch.nn.Parameter(torch.log(scene.scales.to(dev)))
+    rot_raw = torch.nn.Parameter(scene.rotations.to(dev) * 2.0)
+    feats = torch.nn.Parameter(scene.shs.to(dev))
+    screenspace_points = torch.zeros_like(xyz, dtype=xyz.dtype, requires_grad=True, device="cuda") + 0
+    screenspace_points.retain_grad()
+    raster_settings = GaussianRasterizationSettings(
+        image_height=int(cam.height), image_width=int(cam.width), tanfovx=cam.tanfovx, tanfovy=cam.tanfovy,
+        bg=torch.tensor([0.0, 0.0, 0.0], device=dev), scale_modifier=1.0,
+        viewmatrix=cam.world_view_transform.to(dev), projmatrix=cam.full_proj_transform.to(dev),
+        sh_degree=scene.sh_degree, campos=cam.camera_center.to(dev), prefiltered=False, debug=debug)
+    rasterizer = GaussianRasterizer(raster_settings=raster_settings)
+    rendered_image, radii, depth, alpha, rendered_segment = rasterizer(
+        means3D=xyz, means2D=screenspace_points, opacities=torch.sigmoid(opacity_raw), shs=feats,
+        colors_precomp=None, segments=torch.sigmoid(seg_raw), scales=torch.exp(scale_raw),
+        rotations=torch.nn.functional.normalize(rot_raw), cov3D_precomp=None)
+    depth = depth / (depth.max() + 1e-5)
+    loss = rendered_image.mean() + depth.mean() + alpha.mean() + rendered_segment.mean()
+    loss.backward()
+    params = dict(xyz=xyz, opacity=opacity_raw, seg=seg_raw, scale=scale_raw, rot=rot_raw, feats=feats)
+    return rendered_image, radii, screenspace_points, params, rasterizer
+
+
+def test_renderer_style_call_and_grads(gpu_available):
+    scene = synthetic_scene(5000, sh_degree=3, seed=21)
+    cam = orbit_camera(4, 160, 120, 150.0)
+    img, radii, ssp, params, _ = _renderer_style_call(scene, cam)
+    assert img.shape == (3, 120, 160) and radii.dtype == torch.int32
+    vis = radii > 0
+    assert int(vis.sum()) > 1000
+    assert ssp.grad is not None and torch.isfinite(ssp.grad).all()
+    assert float(ssp.grad[vis, :2].abs().sum()) > 0 and float(ssp.grad[~vis].abs().sum()) == 0
+    for n, p in params.items():
+        assert p.grad is not None and torch.isfinite(p.grad).all(), n
+        assert float(p.grad.abs().sum()) > 0, n
+
+
+def test_debug_mode_matches(gpu_available):
+    scene = synthetic_scene(3000, sh_degree=2, seed=22)
+    cam = orbit_camera(5, 128, 96, 120.0)
+    a = _renderer_style_call(scene, cam, debug=False)
+    b = _renderer_style_call(scene, cam, debug=True)
+    assert torch.equal(a[0], b[0])
+    for n in a[3]:
+        assert torch.equal(a[3][n].grad, b[3][n].grad), n
+
+
+def test_mark_visible_matches_oracle(gpu_available, oracle_mod):
+    scene = synthetic_scene(4000, sh_degree=0, seed=23, extent=4.0)
+    cam = orbit_camera(1, 64, 64, 60.0)
+    *_, rasterizer = _renderer_style_call(synthetic_scene(10, sh_degree=0, seed=1), cam)
+    vis = rasterizer.markVisible(scene.means3D.cuda()).cpu().numpy()
+    ref = oracle_mod.mark_visible(scene.means3D, cam.world_view_transform.numpy())
+    np.testing.assert_array_equal(vis, ref)
+    assert 0 < vis.sum() < len(vis)
+
+
+def test_argument_validation(gpu_available):
+    from diff_gaussian_rasterization import GaussianRasterizer
+    cam = orbit_camera(0, 32, 32, 30.0)
+    st = Hn.settings_for(cam, 0, "cuda")
+    r = GaussianRasterizer(st)
+    m = torch.zeros(4, 3, device="cuda")
+    o = torch.ones(4, 1, device="cuda")
+    with pytest.raises(Exception, match="exactly one of either SHs"):
+        r(means3D=m, means2D=m, opacities=o, scales=m, rotations=torch.ones(4, 4, device="cuda"))
+    with pytest.raises(Exception, match="scale/rotation"):
+        r(means3D=m, means2D=m, opacities=o, shs=torch.ones(4, 1, 3, device="cuda"), scales=m)
+    with pytest.raises(RuntimeError, match="means3D must have dimensions"):
+        r(means3D=torch.zeros(4, 2, device="cuda"), means2D=m, opacities=o, shs=torch.ones(4, 1, 3, device="cuda"),
+          scales=m, rotations=torch.ones(4, 4, device="cuda"))
+
+
+def test_side_stream_matches_default_stream(gpu_available):
+    scene = synthetic_scene(4000, sh_degree=3, seed=24)
+    cam = orbit_camera(6, 128, 128, 120.0)
+    a = Hn.run_gsr(scene, cam, want_state=False)
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        b = Hn.run_gsr(scene, cam, want_state=False)
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(a["color"], b["color"])
+
+
+def test_native_library_is_in_tree(gpu_available):
+    """The HIP path is libgsr.so from this repository (no site-packages copy, no fallback)."""
+    from diff_gaussian_rasterization import _C
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    assert os.path.realpath(_C.LIB_PATH).startswith(os.path.realpath(root))
+    maps = open("/proc/self/maps").read()
+    assert os.path.realpath(_C.LIB_PATH) in maps

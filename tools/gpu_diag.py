@@ -76,11 +76,16 @@ def main():
     cases.append(("colors_precomp", sc, cam, dict(colors_precomp=cols)))
     # cov3D precomp from the scene's scale/rot (torch restatement)
     cases.append(("no_segments", sc, cam, dict(use_segments=False)))
+    only = os.environ.get("DIAG_CASES")
     for name, s, c, kw in cases:
+        if only and name not in only.split(","):
+            continue
         try:
             cmp_case(name, s, c, **kw)
         except Exception:
             traceback.print_exc()
+    if os.environ.get("DIAG_NO_MT"):
+        return
     # full-size timing
     sc, cam = config_scene_and_camera("mt")
     from diff_gaussian_rasterization import _RasterizeGaussians
