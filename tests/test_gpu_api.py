@@ -83,7 +83,7 @@ def test_argument_validation(gpu_available):
     r = GaussianRasterizer(st)
     m = torch.zeros(4, 3, device="cuda")
     o = torch.ones(4, 1, device="cuda")
-    with pytest.raises(Exception, match="exactly one of either SHs"):
+    with pytest.raises(Exception, match="excatly one of either SHs"):  # reference's own spelling (:203)
         r(means3D=m, means2D=m, opacities=o, scales=m, rotations=torch.ones(4, 4, device="cuda"))
     with pytest.raises(Exception, match="scale/rotation"):
         r(means3D=m, means2D=m, opacities=o, shs=torch.ones(4, 1, 3, device="cuda"), scales=m)
