@@ -8,27 +8,53 @@
 // loop then broadcasts record j to the wave with v_readlane (scalar operands,
 // no LDS, no block barriers).  Early termination is a wave ballot.
 //
+// Per pair, the four pixel "powers" are computed first and compared with the
+// Gaussian's log-space opacity threshold ln(1/(255*o)) (minus a 1e-3 guard):
+// when no pixel of the tile can reach alpha >= 1/255 the pair is skipped
+// before any exp().  Pairs that pass are decided with the exact test of the
+// reference (expf, alpha >= 1/255), so the skip never changes a result.
+//
 // Backward: instead of the reference's 12 float atomics per (pixel, Gaussian)
-// pair, each lane first sums its 4 pixels in registers, the wave reduces the 12
-// gradient channels with a transposed butterfly (14 cross-lane moves for 12
-// values), and 12 lanes store ONE 48-B record per (tile, Gaussian) instance at
-// the instance's slot.  The per-Gaussian backward kernel sums a Gaussian's
-// slots in fixed order: deterministic, atomic-free gradients.
+// pair, each lane sums its 4 pixels in registers, the wave reduces the 12
+// gradient channels with a transposed butterfly on v_permlane32_swap /
+// v_permlane16_swap / DPP (34 VALU ops, no LDS round trips), and 12 lanes
+// store ONE 48-B record per (tile, Gaussian) instance at the instance's slot.
+// The per-Gaussian backward kernel sums a Gaussian's slots in fixed order:
+// deterministic, atomic-free gradients.
 #include "gsr_internal.h"
 
 // Numerics.  The blend thresholds alpha >= 1/255 and T*(1-alpha) >= 1e-4
 // (forward.cu:352-359) make n_contrib and every contribution knife-edge
-// sensitive to exp(): the full-precision expf (ocml, ~1 ulp, like the
-// reference's CUDA expf) keeps threshold flips against the oracle to ~0 on the
-// parity scenes, where __expf (v_exp_f32 of x*log2e, several ulp at |x|~5)
-// flipped about one pair per 10^7.  GSR_FAST_EXP selects the fast form.
-// The forward blend keeps FMA contraction (errors ~2e-7); the backward replay
-// runs with contraction off so its long recurrences (T /= 1-alpha, accum_rec)
-// round like the reference's sequential code.
+// sensitive to exp(), and the reference's backward recovers T from
+// T_final = 1 - sum(alpha*T) (backward.cu:468), amplifying any last-ulp alpha
+// difference by 1/T_final.  gsr therefore evaluates exp() with gsr_expf below:
+// IEEE operations only (mul, rint, fma, ldexp), so the CPU oracle computes the
+// very same bits (oracle/gsr_oracle.cpp: gsr_expf).  Max error 0.88 ulp,
+// correctly rounded on 99.55% of inputs (tests/test_oracle_golden.py pins it
+// against double-precision exp; the reference's CUDA expf is specified at 2 ulp).
+// GSR_FAST_EXP selects __expf (v_exp_f32, several ulp) for experiments.
+// power, alpha, T and the weight sum run without FMA contraction (see the
+// kernels); only non-amplified sums use explicit FMAs.
+__device__ __forceinline__ float gsr_expf(float x) {
+    const float xc = fminf(fmaxf(x, -104.0f), 88.72283935546875f);
+    const float k = __builtin_rintf(xc * 1.44269502f);
+    float r = __builtin_fmaf(-k, 0.693145751953125f, xc);  // Cody-Waite ln2 = hi + lo
+    r = __builtin_fmaf(-k, 1.42860677e-06f, r);
+    float p = 1.98412701e-04f;                  // 1/7!, Horner with FMAs
+    p = __builtin_fmaf(p, r, 1.38888892e-03f);  // 1/6!
+    p = __builtin_fmaf(p, r, 8.33333377e-03f);  // 1/5!
+    p = __builtin_fmaf(p, r, 4.16666679e-02f);  // 1/4!
+    p = __builtin_fmaf(p, r, 1.66666672e-01f);  // 1/3!
+    p = __builtin_fmaf(p, r, 0.5f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    const float v = __builtin_ldexpf(p, (int)k);
+    return x < -104.0f ? 0.0f : (x > 88.72283935546875f ? __builtin_inff() : v);
+}
 #ifdef GSR_FAST_EXP
 #define GSR_EXP(x) __expf(x)
 #else
-#define GSR_EXP(x) expf(x)
+#define GSR_EXP(x) gsr_expf(x)
 #endif
 
 namespace gsr {
@@ -43,6 +69,15 @@ __device__ __forceinline__ uint32_t bcast_u(uint32_t v, int j) {
 
 constexpr float ALPHA_MIN = 1.0f / 255.0f;  // forward.cu:352
 constexpr float T_MIN = 0.0001f;            // forward.cu:355
+constexpr float POWER_GUARD = 1e-3f;        // skip guard in ln-space (alpha factor e^-0.001)
+
+// Lowest power at which o * exp(power) can still reach 1/255 (minus the guard).
+__device__ __forceinline__ float power_floor(float opacity) {
+#ifdef GSR_NO_SKIP
+    return -INFINITY;
+#endif
+    return -__logf(255.0f * opacity) - POWER_GUARD;
+}
 
 __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ point_list,
@@ -50,22 +85,29 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
                                                    float* __restrict__ out_color, float* __restrict__ out_depth,
                                                    float* __restrict__ out_alpha, float* __restrict__ out_segment,
                                                    uint32_t* __restrict__ n_contrib) {
+    // The backward recovers T from T_final = 1 - sum(alpha*T) (backward.cu:468) and
+    // divides back through every contributor, which amplifies a last-bit difference
+    // in the weight sum by 1/T_final.  power, alpha, T and the weight sum are therefore
+    // rounded exactly as the reference writes them (no contraction); only the
+    // colour/depth/segment sums, which nothing amplifies, use explicit FMAs.
+#pragma clang fp contract(off)
     const int tile = blockIdx.x;
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
     const int px = tx * BX + (lane & 15);
     const int py0 = ty * BY + (lane >> 4);
     const float pfx = (float)px;
-    float pfy[4], T[4], C0[4], C1[4], C2[4], S0[4], S1[4], Dp[4], Wt[4];
+    // T == 0 marks a terminated (or outside) pixel: T only ever holds values >= 1e-4
+    // while blending, and T(1-alpha) = 0 < 1e-4 keeps it out of every later blend.
+    float pfy[4], T[4], Tend[4], C0[4], C1[4], C2[4], S0[4], S1[4], Dp[4], Wt[4];
     uint32_t last[4];
-    bool done[4], inside[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         const int py = py0 + 4 * k;
         pfy[k] = (float)py;
-        inside[k] = px < W && py < H;
-        done[k] = !inside[k];
-        T[k] = 1.0f;
+        const bool inside = px < W && py < H;
+        T[k] = inside ? 1.0f : 0.0f;
+        Tend[k] = 0.0f;
         C0[k] = C1[k] = C2[k] = S0[k] = S1[k] = Dp[k] = Wt[k] = 0.f;
         last[k] = 0;
     }
@@ -73,32 +115,43 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     const int n = (int)(range.y - range.x);
 
     for (int base = 0; base < n; base += 64) {
-        if (!__any(!(done[0] && done[1] && done[2] && done[3]))) break;
+        if (!__any(T[0] > 0.f || T[1] > 0.f || T[2] > 0.f || T[3] > 0.f)) break;
         const int cnt = min(64, n - base);
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra, rc = ra;
+        float pmin = 0.f;
         if (lane < cnt) {
             const uint32_t g = point_list[range.x + base + lane];
             const float4* R = rec + (size_t)g * REC_F4;
             ra = R[0];
             rb = R[1];
             rc = R[2];
+            pmin = power_floor(rb.y);
         }
         for (int j = 0; j < cnt; ++j) {
             const float gx_ = bcast(ra.x, j), gy_ = bcast(ra.y, j);
-            const float ca = bcast(ra.z, j), cb = bcast(ra.w, j), cc = bcast(rb.x, j), op = bcast(rb.y, j);
+            const float ca = bcast(ra.z, j), cb = bcast(ra.w, j), cc = bcast(rb.x, j), pm = bcast(pmin, j);
+            float power[4];
+            bool near = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float dx = gx_ - pfx, dy = gy_ - pfy[k];
+                power[k] = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
+                near = near || (power[k] >= pm && T[k] > 0.f);
+            }
+            if (!__any(near)) continue;
+            const float op = bcast(rb.y, j);
             bool ok[4];
             float alpha[4];
             bool any_ok = false;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float dx = gx_ - pfx, dy = gy_ - pfy[k];
-                const float power = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
-                alpha[k] = fminf(0.99f, op * GSR_EXP(power));
-                bool o = !done[k] && power <= 0.0f && alpha[k] >= ALPHA_MIN;
+                alpha[k] = fminf(0.99f, op * GSR_EXP(power[k]));
+                const bool o = power[k] <= 0.0f && alpha[k] >= ALPHA_MIN;
                 const float test_T = T[k] * (1.f - alpha[k]);
-                const bool term = o && test_T < T_MIN;
-                done[k] = done[k] || term;
-                ok[k] = o && !term;
+                const bool term = o && T[k] > 0.f && test_T < T_MIN;
+                Tend[k] = term ? T[k] : Tend[k];
+                ok[k] = o && test_T >= T_MIN;
+                T[k] = term ? 0.f : T[k];
                 any_ok = any_ok || ok[k];
             }
             if (!__any(any_ok)) continue;
@@ -107,15 +160,14 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
             const uint32_t contributor = (uint32_t)(base + j + 1);
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float a = ok[k] ? alpha[k] : 0.f;
-                const float aT = a * T[k];
-                C0[k] += cr * a * T[k];
-                C1[k] += cg * a * T[k];
-                C2[k] += cbl * a * T[k];
-                Wt[k] += aT;
-                Dp[k] += dep * a * T[k];
-                S0[k] += s0 * a * T[k];
-                S1[k] += s1 * a * T[k];
+                const float aT = (ok[k] ? alpha[k] : 0.f) * T[k];
+                C0[k] = __builtin_fmaf(cr, aT, C0[k]);
+                C1[k] = __builtin_fmaf(cg, aT, C1[k]);
+                C2[k] = __builtin_fmaf(cbl, aT, C2[k]);
+                Wt[k] += aT;  // weight += alpha * T (forward.cu:364), exact rounding
+                Dp[k] = __builtin_fmaf(dep, aT, Dp[k]);
+                S0[k] = __builtin_fmaf(s0, aT, S0[k]);
+                S1[k] = __builtin_fmaf(s1, aT, S1[k]);
                 T[k] = ok[k] ? T[k] * (1.f - alpha[k]) : T[k];
                 last[k] = ok[k] ? contributor : last[k];
             }
@@ -126,11 +178,13 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         n_contrib[(size_t)tile * TILE_PIX + k * 64 + lane] = last[k];
-        if (!inside[k]) continue;
-        const size_t pix = (size_t)(py0 + 4 * k) * W + px;
-        out_color[pix] = C0[k] + T[k] * bg0;
-        out_color[HW + pix] = C1[k] + T[k] * bg1;
-        out_color[2 * HW + pix] = C2[k] + T[k] * bg2;
+        const int py = py0 + 4 * k;
+        if (!(px < W && py < H)) continue;
+        const float Tf = T[k] > 0.f ? T[k] : Tend[k];
+        const size_t pix = (size_t)py * W + px;
+        out_color[pix] = C0[k] + Tf * bg0;
+        out_color[HW + pix] = C1[k] + Tf * bg1;
+        out_color[2 * HW + pix] = C2[k] + Tf * bg2;
         out_alpha[pix] = Wt[k];
         out_depth[pix] = Dp[k];
         out_segment[pix] = S0[k];
@@ -138,41 +192,59 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     }
 }
 
-// Transposed butterfly: v[12] per lane -> the wave-wide sum of channel vidx in
-// every lane with (lane & 3) == 0 && valid.
+template <int CTRL>
+__device__ __forceinline__ float dpp(float v) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Transposed butterfly over the wave: v[12] per lane -> lane l (with (l & 3) == 0
+// and valid) holds the wave-wide sum of channel vidx.  xor-32 and xor-16 halves
+// are exchanged by v_permlane32_swap / v_permlane16_swap (no selects: the swap
+// itself routes each half), xor-8 by DPP row_ror:8, xor-4 by row_half_mirror
+// (partner differs in bit 2), the last two steps by quad_perm DPP adds.
 __device__ __forceinline__ float wave_reduce12(float v[12], int lane, int& vidx, bool& valid) {
-    const bool h32 = lane & 32, h16 = lane & 16, h8 = lane & 8, h4 = lane & 4;
+    float s6[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) {
-        const float send = h32 ? v[i] : v[i + 6];
-        const float keep = h32 ? v[i + 6] : v[i];
-        v[i] = keep + __shfl_xor(send, 32, 64);
+        auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v[i]), __float_as_uint(v[i + 6]), false, false);
+        s6[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // lanes <32: ch i, lanes >=32: ch i+6
     }
+    float s3[4];
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-        const float send = h16 ? v[i] : v[i + 3];
-        const float keep = h16 ? v[i + 3] : v[i];
-        v[i] = keep + __shfl_xor(send, 16, 64);
+        auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(s6[i]), __float_as_uint(s6[i + 3]), false, false);
+        s3[i] = __uint_as_float(r[0]) + __uint_as_float(r[1]);  // row q holds ch 3q + i
     }
-    v[3] = 0.f;
+    s3[3] = 0.f;
+    const bool h8 = lane & 8, h4 = lane & 4;
+    float s2[2];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
-        const float send = h8 ? v[i] : v[i + 2];
-        const float keep = h8 ? v[i + 2] : v[i];
-        v[i] = keep + __shfl_xor(send, 8, 64);
+        const float send = h8 ? s3[i] : s3[i + 2];
+        const float keep = h8 ? s3[i + 2] : s3[i];
+        s2[i] = keep + dpp<0x128>(send);  // row_ror:8 == xor 8 inside a row
     }
-    {
-        const float send = h4 ? v[0] : v[1];
-        const float keep = h4 ? v[1] : v[0];
-        v[0] = keep + __shfl_xor(send, 4, 64);
-    }
-    float r = v[0];
-    r += __shfl_xor(r, 2, 64);
-    r += __shfl_xor(r, 1, 64);
+    const float send = h4 ? s2[0] : s2[1];
+    const float keep = h4 ? s2[1] : s2[0];
+    float r = keep + dpp<0x141>(send);  // row_half_mirror: partner differs in bit 2
+    r += dpp<0x4E>(r);                  // quad_perm [2,3,0,1]
+    r += dpp<0xB1>(r);                  // quad_perm [1,0,3,2]
     const int w = (h8 ? 2 : 0) + (h4 ? 1 : 0);
-    vidx = (h32 ? 6 : 0) + (h16 ? 3 : 0) + w;
+    vidx = 3 * (lane >> 4) + w;
     valid = ((lane & 3) == 0) && w < 3;
     return r;
+}
+
+// q = num / den, from v_rcp_f32 plus one Newton correction of the quotient
+// (within 1 ulp of the IEEE quotient; 4 ops instead of the ~10 of div_scale/fmas/fixup).
+__device__ __forceinline__ float fdiv(float num, float den) {
+#ifdef GSR_IEEE_DIV
+    return num / den;
+#endif
+    const float r = __builtin_amdgcn_rcpf(den);
+    const float q = num * r;
+    const float e = __builtin_fmaf(-q, den, num);
+    return __builtin_fmaf(e, r, q);
 }
 
 __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const uint2* __restrict__ ranges,
@@ -196,9 +268,13 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
     const size_t HW = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
 
+    // Per-pixel replay state.  The reference keeps (last_alpha, last_color, ...) and
+    // folds them into accum_rec at the NEXT contributor (backward.cu:567,583,598,604);
+    // here the same expression a*c + (1-a)*accum is evaluated right after the
+    // contributor that owns (a, c) -- identical operands and operations, one step
+    // earlier -- so no last_* registers are needed.
     float pfy[4], T[4], Tfin[4], dp0[4], dp1[4], dp2[4], ds0[4], ds1[4], dd[4], da[4], bgdot[4];
-    float ar0[4], ar1[4], ar2[4], as0[4], as1[4], ad[4], aa[4], la[4], lc0[4], lc1[4], lc2[4], ls0[4], ls1[4],
-        ld[4];
+    float ar0[4], ar1[4], ar2[4], as0[4], as1[4], ad[4], aa[4];
     uint32_t lastc[4];
     uint32_t maxlast = 0;
 #pragma unroll
@@ -206,7 +282,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
         const int py = py0 + 4 * k;
         pfy[k] = (float)py;
         const bool inside = px < W && py < H;
-        const size_t pix = (size_t)py * W + px;
+        const size_t pix = inside ? (size_t)py * W + px : 0;
         lastc[k] = inside ? n_contrib[(size_t)tile * TILE_PIX + k * 64 + lane] : 0u;
         Tfin[k] = inside ? 1.f - alphas[pix] : 0.f;
         T[k] = Tfin[k];
@@ -223,7 +299,6 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
         bgd += bg2 * dp2[k];
         bgdot[k] = bgd;
         ar0[k] = ar1[k] = ar2[k] = as0[k] = as1[k] = ad[k] = aa[k] = 0.f;
-        la[k] = lc0[k] = lc1[k] = lc2[k] = ls0[k] = ls1[k] = ld[k] = 0.f;
         maxlast = max(maxlast, lastc[k]);
     }
 #pragma unroll
@@ -247,6 +322,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
         const int cnt = min(64, top);
         float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra, rc = ra;
         uint32_t uslot = 0;
+        float pmin = 0.f;
         if (lane < cnt) {
             const uint32_t kidx = range.x + (uint32_t)(top - 1 - lane);
             const uint32_t g = point_list[kidx];
@@ -255,25 +331,37 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
             ra = R[0];
             rb = R[1];
             rc = R[2];
+            pmin = power_floor(rb.y);
         }
         for (int j = 0; j < cnt; ++j) {
             const uint32_t p = (uint32_t)(top - 1 - j);
             const uint32_t u = bcast_u(uslot, j);
             float* dst = contrib + (size_t)u * 12;
             const float gx_ = bcast(ra.x, j), gy_ = bcast(ra.y, j);
-            const float ca = bcast(ra.z, j), cb = bcast(ra.w, j), cc = bcast(rb.x, j), op = bcast(rb.y, j);
-            bool ok[4];
-            float G[4], alpha[4], dxs[4], dys[4];
-            bool any_ok = false;
+            const float ca = bcast(ra.z, j), cb = bcast(ra.w, j), cc = bcast(rb.x, j), pm = bcast(pmin, j);
+            float power[4], dxs[4], dys[4];
+            bool near = false;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float dx = gx_ - pfx, dy = gy_ - pfy[k];
                 dxs[k] = dx;
                 dys[k] = dy;
-                const float power = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
-                G[k] = GSR_EXP(power);
+                power[k] = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
+                near = near || (p < lastc[k] && power[k] >= pm);
+            }
+            if (!__any(near)) {
+                if (lane < 12) dst[lane] = 0.f;
+                continue;
+            }
+            const float op = bcast(rb.y, j);
+            bool ok[4];
+            float G[4], alpha[4];
+            bool any_ok = false;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                G[k] = GSR_EXP(power[k]);
                 alpha[k] = fminf(0.99f, op * G[k]);
-                ok[k] = p < lastc[k] && power <= 0.0f && alpha[k] >= ALPHA_MIN;
+                ok[k] = p < lastc[k] && power[k] <= 0.0f && alpha[k] >= ALPHA_MIN;
                 any_ok = any_ok || ok[k];
             }
             if (!__any(any_ok)) {
@@ -290,56 +378,45 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
                 const bool o = ok[k];
                 const float a = alpha[k];
                 const float one_m = 1.f - a;
-                const float Tn = o ? T[k] / one_m : T[k];
-                T[k] = Tn;
+                const float Tn = fdiv(T[k], one_m);
                 const float dch = a * Tn;
-                // colour
-                const float nar0 = la[k] * lc0[k] + (1.f - la[k]) * ar0[k];
-                const float nar1 = la[k] * lc1[k] + (1.f - la[k]) * ar1[k];
-                const float nar2 = la[k] * lc2[k] + (1.f - la[k]) * ar2[k];
                 float dopa = 0.f;
-                dopa += (c0 - nar0) * dp0[k];
-                dopa += (c1 - nar1) * dp1[k];
-                dopa += (c2 - nar2) * dp2[k];
-                // segment
-                const float nas0 = la[k] * ls0[k] + (1.f - la[k]) * as0[k];
-                const float nas1 = la[k] * ls1[k] + (1.f - la[k]) * as1[k];
-                dopa += (s0 - nas0) * ds0[k];
-                dopa += (s1 - nas1) * ds1[k];
-                // depth
-                const float nad = la[k] * ld[k] + (1.f - la[k]) * ad[k];
-                dopa += (dep - nad) * dd[k];
-                // alpha (weight sum)
-                const float naa = la[k] + (1.f - la[k]) * aa[k];
-                dopa += (1.f - naa) * da[k];
+                dopa += (c0 - ar0[k]) * dp0[k];
+                dopa += (c1 - ar1[k]) * dp1[k];
+                dopa += (c2 - ar2[k]) * dp2[k];
+                dopa += (s0 - as0[k]) * ds0[k];
+                dopa += (s1 - as1[k]) * ds1[k];
+                dopa += (dep - ad[k]) * dd[k];
+                dopa += (1.f - aa[k]) * da[k];
                 dopa *= Tn;
-                if (use_bg) dopa += (-Tfin[k] / one_m) * bgdot[k];
-                const float dL_dG = op * dopa;
+                if (use_bg) dopa += (-Tfin[k] * __builtin_amdgcn_rcpf(one_m)) * bgdot[k];
+                const float dopa_m = o ? dopa : 0.f;
+                const float dch_m = o ? dch : 0.f;
+                const float dL_dG = op * dopa_m;
                 const float gdx = G[k] * dxs[k], gdy = G[k] * dys[k];
                 const float dG_ddelx = -gdx * ca - gdy * cb;
                 const float dG_ddely = -gdy * cc - gdx * cb;
-                if (o) {
-                    acc[0] += dch * dp0[k];
-                    acc[1] += dch * dp1[k];
-                    acc[2] += dch * dp2[k];
-                    acc[3] += dch * ds0[k];
-                    acc[4] += dch * ds1[k];
-                    acc[5] += dch * dd[k];
-                    acc[6] += dL_dG * dG_ddelx * ddelx_dx;
-                    acc[7] += dL_dG * dG_ddely * ddely_dy;
-                    acc[8] += -0.5f * gdx * dxs[k] * dL_dG;
-                    acc[9] += -0.5f * gdx * dys[k] * dL_dG;
-                    acc[10] += -0.5f * gdy * dys[k] * dL_dG;
-                    acc[11] += G[k] * dopa;
-                    ar0[k] = nar0; ar1[k] = nar1; ar2[k] = nar2;
-                    as0[k] = nas0; as1[k] = nas1;
-                    ad[k] = nad;
-                    aa[k] = naa;
-                    lc0[k] = c0; lc1[k] = c1; lc2[k] = c2;
-                    ls0[k] = s0; ls1[k] = s1;
-                    ld[k] = dep;
-                    la[k] = a;
-                }
+                acc[0] += dch_m * dp0[k];
+                acc[1] += dch_m * dp1[k];
+                acc[2] += dch_m * dp2[k];
+                acc[3] += dch_m * ds0[k];
+                acc[4] += dch_m * ds1[k];
+                acc[5] += dch_m * dd[k];
+                acc[6] += dL_dG * dG_ddelx * ddelx_dx;
+                acc[7] += dL_dG * dG_ddely * ddely_dy;
+                acc[8] += -0.5f * gdx * dxs[k] * dL_dG;
+                acc[9] += -0.5f * gdx * dys[k] * dL_dG;
+                acc[10] += -0.5f * gdy * dys[k] * dL_dG;
+                acc[11] += G[k] * dopa_m;
+                // fold this contributor into the accumulators seen by the next one (front side)
+                ar0[k] = o ? a * c0 + one_m * ar0[k] : ar0[k];
+                ar1[k] = o ? a * c1 + one_m * ar1[k] : ar1[k];
+                ar2[k] = o ? a * c2 + one_m * ar2[k] : ar2[k];
+                as0[k] = o ? a * s0 + one_m * as0[k] : as0[k];
+                as1[k] = o ? a * s1 + one_m * as1[k] : as1[k];
+                ad[k] = o ? a * dep + one_m * ad[k] : ad[k];
+                aa[k] = o ? a + one_m * aa[k] : aa[k];
+                T[k] = o ? Tn : T[k];
             }
             int vidx;
             bool valid;

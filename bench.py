@@ -112,7 +112,8 @@ def main():
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=device)
 
-    from gsr_tools.scene import config_scene_and_camera, CONFIGS
+    from gsr_tools.scene import config_scene_and_camera
+    from gsr_tools import dp
     import diff_gaussian_rasterization as dgr
     from diff_gaussian_rasterization import _C
 
@@ -143,9 +144,7 @@ def main():
         g = torch.autograd.grad([color, depth, alpha, segment],
                                 inputs, [ups["color"], ups["depth"], ups["alpha"], ups["segment"]])
         if dist is not None:
-            arena = g[0]._base
-            assert arena is not None and arena.data_ptr() == g[0].data_ptr()
-            dist.all_reduce(arena.narrow(0, 0, lay["bucket"][1]))
+            dp.allreduce_bucket(dp.arena_of(g[0]), P, shs.shape[1])
         return g
 
     for _ in range(args.warmup):

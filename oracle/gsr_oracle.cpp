@@ -178,6 +178,7 @@ struct State {
     std::vector<uint32_t> n_contrib;  // [H*W]
     std::vector<float> alpha;         // out_alpha copy [H*W]
     std::vector<float> segments;      // [P,2] (zeros if absent)
+    std::vector<float> gabs;          // [P,12] sum of |per-pixel gradient terms| (after backward)
 };
 
 // forward.cu:20-71
@@ -259,11 +260,41 @@ static uint32_t getHigherMsb(uint32_t n) {
 
 static std::string g_err;
 
+// exp() of the blend (forward.cu:351, backward.cu:547).  The reference calls CUDA's
+// expf (2 ulp); gsr's kernels and this oracle share gsr_expf: IEEE operations only
+// (mul, rint, fma, ldexp), max 0.88 ulp, so both compute identical bits and the
+// knife-edge blend decisions (alpha >= 1/255, T(1-alpha) >= 1e-4) agree exactly.
+// g_exp_libm = 1 switches to the C library's expf (noise-floor studies).
+static int g_exp_libm = 0;
+static inline float gsr_expf(float x) {
+    const float xc = std::fmin(std::fmax(x, -104.0f), 88.72283935546875f);
+    const float k = std::rint(xc * 1.44269502f);
+    float r = std::fma(-k, 0.693145751953125f, xc);
+    r = std::fma(-k, 1.42860677e-06f, r);
+    float p = 1.98412701e-04f;
+    p = std::fma(p, r, 1.38888892e-03f);
+    p = std::fma(p, r, 8.33333377e-03f);
+    p = std::fma(p, r, 4.16666679e-02f);
+    p = std::fma(p, r, 1.66666672e-01f);
+    p = std::fma(p, r, 0.5f);
+    p = std::fma(p, r, 1.0f);
+    p = std::fma(p, r, 1.0f);
+    const float v = std::ldexp(p, (int)k);
+    return x < -104.0f ? 0.0f : (x > 88.72283935546875f ? INFINITY : v);
+}
+static inline float oracle_exp(float x) { return g_exp_libm ? std::exp(x) : gsr_expf(x); }
+// 1: emulate the reference's fp32 accumulation (one fixed order of its atomics)
+static int g_acc32 = 0;
+
 }  // namespace
 
 extern "C" {
 
 const char* oracle_last_error(void) { return g_err.c_str(); }
+
+void oracle_set_acc32(int on) { g_acc32 = on; }
+void oracle_set_exp_libm(int on) { g_exp_libm = on; }
+float oracle_expf(float x) { return gsr_expf(x); }
 
 int oracle_num_threads(void) {
 #ifdef _OPENMP
@@ -435,7 +466,7 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
                     const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
                     const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                     if (power > 0.0f) continue;
-                    const float alpha = std::min(0.99f, co[3] * std::exp(power));
+                    const float alpha = std::min(0.99f, co[3] * oracle_exp(power));
                     if (alpha < 1.0f / 255.0f) continue;
                     const float test_T = Tr * (1 - alpha);
                     if (test_T < 0.0001f) break;  // done = true
@@ -482,6 +513,7 @@ long oracle_get(void* h, const char* name, void* dst) {
     if (n == "point_list") return cp(st->point_list.data(), st->point_list.size() * 4, st->point_list.size());
     if (n == "ranges") return cp(st->ranges.data(), st->ranges.size() * 4, st->ranges.size());
     if (n == "n_contrib") return cp(st->n_contrib.data(), st->n_contrib.size() * 4, st->n_contrib.size());
+    if (n == "gabs") return cp(st->gabs.data(), st->gabs.size() * 4, st->gabs.size());
     g_err = "unknown field " + n;
     return -1;
 }
@@ -507,7 +539,7 @@ int oracle_backward(void* h, const OracleInputs* in, const float* dL_dpix, const
     const float* segs = st->segments.data();
     // fp64 accumulation: the reference sums with atomicAdd in arbitrary order, so
     // the exact sum of the fp32 per-pixel terms is the centre of its outputs.
-    std::vector<double> contrib((size_t)I * 12, 0.0);
+    std::vector<double> contrib((size_t)I * 12, 0.0), cabs((size_t)I * 12, 0.0);
     const float ddelx_dx = 0.5 * W, ddely_dy = 0.5 * H;
 
     // renderCUDA backward (backward.cu:414-639)
@@ -542,32 +574,38 @@ int oracle_backward(void* h, const OracleInputs* in, const float* dL_dpix, const
                     const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
                     const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                     if (power > 0.0f) continue;
-                    const float G = std::exp(power);
+                    const float G = oracle_exp(power);
                     const float alpha = std::min(0.99f, co[3] * G);
                     if (alpha < 1.0f / 255.0f) continue;
                     Tr = Tr / (1.f - alpha);
                     const float dchannel_dcolor = alpha * Tr;
                     double* cb = &contrib[(size_t)k * 12];
+                    double* ab = &cabs[(size_t)k * 12];
+                    auto ADD = [&](int i, float t) {
+                        if (g_acc32) cb[i] = (double)((float)cb[i] + t);
+                        else cb[i] += t;
+                        ab[i] += std::fabs((double)t);
+                    };
                     float dL_dopa = 0.0f;
                     for (int ch = 0; ch < NCH; ++ch) {
                         const float c = colors[g * NCH + ch];
                         accum_rec[ch] = last_alpha * last_color[ch] + (1.f - last_alpha) * accum_rec[ch];
                         last_color[ch] = c;
                         dL_dopa += (c - accum_rec[ch]) * dL_dpixel[ch];
-                        cb[0 + ch] += dchannel_dcolor * dL_dpixel[ch];
+                        ADD(0 + ch, dchannel_dcolor * dL_dpixel[ch]);
                     }
                     for (int ch = 0; ch < NCLS; ++ch) {
                         const float c_s = segs[g * NCLS + ch];
                         accum_seg[ch] = last_alpha * last_seg[ch] + (1.f - last_alpha) * accum_seg[ch];
                         last_seg[ch] = c_s;
                         dL_dopa += (c_s - accum_seg[ch]) * dL_dseg[ch];
-                        cb[3 + ch] += dchannel_dcolor * dL_dseg[ch];
+                        ADD(3 + ch, dchannel_dcolor * dL_dseg[ch]);
                     }
                     const float c_d = st->depths[g];
                     accum_depth = last_alpha * last_depth + (1.f - last_alpha) * accum_depth;
                     last_depth = c_d;
                     dL_dopa += (c_d - accum_depth) * dL_dd;
-                    cb[5] += dchannel_dcolor * dL_dd;
+                    ADD(5, dchannel_dcolor * dL_dd);
                     accum_alpha = last_alpha + (1.f - last_alpha) * accum_alpha;
                     dL_dopa += (1 - accum_alpha) * dL_da;
                     dL_dopa *= Tr;
@@ -579,20 +617,25 @@ int oracle_backward(void* h, const OracleInputs* in, const float* dL_dpix, const
                     const float gdx = G * dx, gdy = G * dy;
                     const float dG_ddelx = -gdx * co[0] - gdy * co[1];
                     const float dG_ddely = -gdy * co[2] - gdx * co[1];
-                    cb[6] += dL_dG * dG_ddelx * ddelx_dx;
-                    cb[7] += dL_dG * dG_ddely * ddely_dy;
-                    cb[8] += -0.5f * gdx * dx * dL_dG;
-                    cb[9] += -0.5f * gdx * dy * dL_dG;
-                    cb[10] += -0.5f * gdy * dy * dL_dG;
-                    cb[11] += G * dL_dopa;
+                    ADD(6, dL_dG * dG_ddelx * ddelx_dx);
+                    ADD(7, dL_dG * dG_ddely * ddely_dy);
+                    ADD(8, -0.5f * gdx * dx * dL_dG);
+                    ADD(9, -0.5f * gdx * dy * dL_dG);
+                    ADD(10, -0.5f * gdy * dy * dL_dG);
+                    ADD(11, G * dL_dopa);
                 }
             }
     }
     // Gather per-gaussian sums: [dcolor3 dseg2 ddepth dmean2D.xy dconic.xyw dopacity]
     std::vector<double> gsum_d((size_t)P * 12, 0.0);
+    st->gabs.assign((size_t)P * 12, 0.f);
     for (int k = 0; k < I; ++k) {
         const uint32_t g = st->point_list[k];
-        for (int j = 0; j < 12; ++j) gsum_d[(size_t)g * 12 + j] += contrib[(size_t)k * 12 + j];
+        for (int j = 0; j < 12; ++j) {
+            double& d = gsum_d[(size_t)g * 12 + j];
+            d = g_acc32 ? (double)((float)d + (float)contrib[(size_t)k * 12 + j]) : d + contrib[(size_t)k * 12 + j];
+            st->gabs[(size_t)g * 12 + j] += (float)cabs[(size_t)k * 12 + j];
+        }
     }
     std::vector<float> gsum(gsum_d.begin(), gsum_d.end());
     std::vector<float> ddepth(P);

@@ -53,6 +53,10 @@ def lib():
         L.oracle_mark_visible.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_num_threads.restype = ctypes.c_int
         L.oracle_set_num_threads.argtypes = [ctypes.c_int]
+        L.oracle_set_acc32.argtypes = [ctypes.c_int]
+        L.oracle_set_exp_libm.argtypes = [ctypes.c_int]
+        L.oracle_expf.argtypes = [ctypes.c_float]
+        L.oracle_expf.restype = ctypes.c_float
         _lib = L
     return _lib
 
@@ -73,8 +77,24 @@ def _ptr(a):
 _FIELD_DTYPES = {
     "depths": np.float32, "means2D": np.float32, "cov3D": np.float32, "conic_opacity": np.float32,
     "rgb": np.float32, "clamped": np.uint8, "tiles_touched": np.uint32, "point_offsets": np.uint32,
-    "keys": np.uint64, "point_list": np.uint32, "ranges": np.uint32, "n_contrib": np.uint32,
+    "keys": np.uint64, "point_list": np.uint32, "ranges": np.uint32, "n_contrib": np.uint32, "gabs": np.float32,
 }
+
+
+def set_acc32(on):
+    """True: accumulate per-pixel gradient terms in fp32 in one fixed order (emulates one
+    run of the reference's atomicAdds); False (default): exact (fp64) sums."""
+    lib().oracle_set_acc32(int(bool(on)))
+
+
+def set_exp_libm(on):
+    """True: blend with the C library's expf instead of gsr_expf (noise-floor studies)."""
+    lib().oracle_set_exp_libm(int(bool(on)))
+
+
+def expf(x):
+    """The blend exponential shared by the oracle and the HIP kernels (gsr_expf)."""
+    return float(lib().oracle_expf(float(x)))
 
 
 class OracleRun:

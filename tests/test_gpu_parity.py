@@ -2,17 +2,17 @@
 
 Tolerances (north_star: bit-exact tile/key indexing, 1e-5 fp32 on images and grads):
   * integer outputs -- radii, tiles_touched, num_rendered, point_list (the sorted
-    (tile, depth, gaussian) order), ranges -- are compared bit-exact;
-  * n_contrib: at most 1e-4 of the pixels may differ (knife-edge threshold flips,
-    see below); on every scene here the measured count is 0;
+    (tile, depth, gaussian) order), ranges and per-pixel n_contrib -- bit-exact;
   * images (color, depth, alpha, segment): |gsr - oracle| <= 1e-5 * max(1, |oracle|)
-    per pixel, except at most 1e-4 of the pixels, which must stay within 5e-2 --
-    the blend thresholds alpha >= 1/255 and T(1-alpha) >= 1e-4 (forward.cu:352-359)
-    flip when two correct exp() implementations differ in the last ulp, and one
-    flipped pair moves a pixel by at most one blend step (alpha*T*value);
-  * gradients: |gsr - oracle| <= 1e-5 * max(1, max|oracle|) per tensor (normwise),
-    except at most 1e-4 of the elements, which must stay within 1e-3 * max(1, max|oracle|)
-    (the same threshold flips, seen through the backward).
+    for every pixel;
+  * gradients: |gsr - oracle| <= 1e-5 * max(1, max|oracle|) for every element
+    (normwise per tensor; the oracle sums gradient terms exactly, the reference's
+    atomicAdd order is arbitrary).
+The kernels and the oracle share one IEEE-only exp (gsr_expf), so the knife-edge
+blend decisions (alpha >= 1/255, T(1-alpha) >= 1e-4, forward.cu:352-359) agree
+exactly; the *_OUTLIER_* budgets below are therefore 0.  (With the C library's
+expf in the oracle instead, up to ~2e-3 of the gradient elements move by up to
+1.4e-4 at the metric config: tools/noise_diag.py)
 """
 import math
 
@@ -26,8 +26,8 @@ from gsr_tools.scene import (Scene, config_scene_and_camera, synthetic_scene, or
 
 pytestmark = pytest.mark.gpu
 
-IMG_TOL, IMG_OUTLIER_FRAC, IMG_OUTLIER_MAX = 1e-5, 1e-4, 5e-2
-GRAD_TOL, GRAD_OUTLIER_FRAC, GRAD_OUTLIER_MAX = 1e-5, 1e-4, 1e-3
+IMG_TOL, IMG_OUTLIER_FRAC, IMG_OUTLIER_MAX = 1e-5, 0.0, 1e-5
+GRAD_TOL, GRAD_OUTLIER_FRAC, GRAD_OUTLIER_MAX = 1e-5, 0.0, 1e-5
 
 
 def assert_integer_parity(g, r):
@@ -36,8 +36,7 @@ def assert_integer_parity(g, r):
     np.testing.assert_array_equal(g["tiles_touched"].astype(np.uint32), r["tiles_touched"])
     np.testing.assert_array_equal(g["point_list"].astype(np.uint32), r["point_list"])
     np.testing.assert_array_equal(g["ranges"].astype(np.uint32), r["ranges"])
-    mism = int((g["n_contrib"].astype(np.uint32) != r["n_contrib"]).sum())
-    assert mism <= IMG_OUTLIER_FRAC * r["n_contrib"].size, f"n_contrib mismatches: {mism}"
+    np.testing.assert_array_equal(g["n_contrib"].astype(np.uint32), r["n_contrib"])
 
 
 def assert_image_parity(g, r):
