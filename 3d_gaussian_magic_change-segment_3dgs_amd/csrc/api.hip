@@ -207,23 +207,29 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
         uint32_t* kout = (passes % 2 == 0) ? kin : kalt;
         uint32_t* ktmp = (passes % 2 == 0) ? kalt : kin;
         {
+            // key = tile, payload = (instance slot u, Gaussian id): the slot orders ties by
+            // (depth, gaussian); the id travels along so point_list needs no gather.
             StageScope sc(GSR_STAGE_TILE_SORT, st);
             launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout, at<uint32_t>(b, BL.slot_vals),
-                              I, bits, at<uint32_t>(b, BL.hist), at<uint32_t>(b, BL.parts), st);
+                              I, bits, at<uint32_t>(b, BL.hist), at<uint32_t>(b, BL.parts), st,
+                              at<uint32_t>(b, BL.slot_gid), at<uint32_t>(b, BL.gid_alt),
+                              at<uint32_t>(b, BL.point_list));
         }
         GSR_STAGE("tile sort");
         point_list = at<uint32_t>(b, BL.point_list);
         {
             StageScope sc(GSR_STAGE_RANGES, st);
-            launch_finalize(I, kout, at<uint32_t>(b, BL.slot_vals), at<uint32_t>(b, BL.slot_gid), point_list, ranges,
-                            st);
+            launch_finalize(I, kout, ranges, st);
         }
         GSR_STAGE("tile ranges");
     }
+    uint32_t* order = at<uint32_t>(im, IL.order);
     {
         StageScope sc(GSR_STAGE_RENDER_FWD, st);
-        launch_render_forward(s->W, s->H, IL.gx, IL.gy, ranges, point_list, g ? at<float4>(g, GL.rec) : nullptr,
-                              s->bg, out_color, out_depth, out_alpha, out_segment, at<uint32_t>(im, IL.n_contrib), st);
+        launch_tile_order(ranges, T, order, st);
+        launch_render_forward(s->W, s->H, IL.gx, IL.gy, order, ranges, point_list,
+                              g ? at<float4>(g, GL.rec) : nullptr, s->bg, out_color, out_depth, out_alpha,
+                              out_segment, at<uint32_t>(im, IL.n_contrib), st);
     }
     GSR_STAGE("render");
     return 0;
@@ -256,7 +262,7 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
         contrib = reinterpret_cast<float*>(aligned_base(scratch));
         {
             StageScope sc(GSR_STAGE_RENDER_BWD, st);
-            launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint2>(im, IL.ranges),
+            launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order), at<uint2>(im, IL.ranges),
                                    at<uint32_t>(b, BL.point_list), at<uint32_t>(b, BL.slot_vals),
                                    at<float4>(g, GL.rec), s->bg, alpha, at<uint32_t>(im, IL.n_contrib), dL_dcolor,
                                    dL_dsegment, dL_ddepth, dL_dalpha, contrib, st);

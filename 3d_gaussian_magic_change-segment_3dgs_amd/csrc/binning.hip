@@ -152,10 +152,12 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_upsweep(const uint32_t* 
 // Stable scatter.  Elements are ranked round by round (256 per round, in index
 // order); inside a round, a wave64 multi-split by ballots gives each element its
 // rank among equal digits of its wave, and per-wave digit counts in LDS order the
-// four waves.  vals_in == NULL means value = element index.
+// four waves.  vals_in == NULL means value = element index.  An optional second
+// payload word (vals2) travels with the pair (NULL = none).
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
-    uint32_t* __restrict__ vals_out, size_t n, int shift, int bits, const uint32_t* __restrict__ hist) {
+    uint32_t* __restrict__ vals_out, size_t n, int shift, int bits, const uint32_t* __restrict__ hist,
+    const uint32_t* __restrict__ vals2_in, uint32_t* __restrict__ vals2_out) {
     __shared__ uint32_t base_off[RADIX];
     __shared__ uint32_t wcnt[4][RADIX];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -168,10 +170,11 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
         for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
         const size_t idx = base + (size_t)r * SORT_THREADS + tid;
         const bool valid = idx < n;
-        uint32_t key = 0, val = 0, digit = 0;
+        uint32_t key = 0, val = 0, val2 = 0, digit = 0;
         if (valid) {
             key = keys_in[idx];
             val = vals_in ? vals_in[idx] : (uint32_t)idx;
+            if (vals2_in) val2 = vals2_in[idx];
             digit = (key >> shift) & mask;
         }
         uint64_t peers = __ballot(valid);
@@ -190,6 +193,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
             for (int w = 0; w < wid; ++w) pos += wcnt[w][digit];
             keys_out[pos] = key;
             vals_out[pos] = val;
+            if (vals2_out) vals2_out[pos] = val2;
         }
         __syncthreads();
         base_off[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
@@ -222,17 +226,48 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
         }
 }
 
-// point_list[k] = gaussian of sorted instance k; tile ranges [first, last+1).
+// Tile ranges [first, last+1) from the sorted tile keys (identifyTileRanges,
+// rasterizer_impl.cu:113-138).
 __global__ void __launch_bounds__(256) k_finalize(size_t I, const uint32_t* __restrict__ tkeys,
-                                                  const uint32_t* __restrict__ slot_vals,
-                                                  const uint32_t* __restrict__ slot_gid,
-                                                  uint32_t* __restrict__ point_list, uint2* __restrict__ ranges) {
+                                                  uint2* __restrict__ ranges) {
     const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= I) return;
-    point_list[k] = slot_gid[slot_vals[k]];
     const uint32_t t = tkeys[k];
     if (k == 0 || tkeys[k - 1] != t) ranges[t].x = (uint32_t)k;
     if (k == I - 1 || tkeys[k + 1] != t) ranges[t].y = (uint32_t)(k + 1);
+}
+
+// Heavy-first tile schedule for the render kernels: tiles bucketed by the bit
+// length of their instance count, longest bucket first.  The hardware dispatcher
+// hands workgroups out in index order as slots free up, so issuing the heavy
+// tiles first turns it into a longest-processing-time-first scheduler (the
+// natural row-major order leaves the dense centre tiles for the end).  Order
+// within a bucket is arbitrary: it changes timing only, never a result.
+__global__ void __launch_bounds__(1024) k_tile_order(const uint2* __restrict__ ranges, int T,
+                                                     uint32_t* __restrict__ order) {
+    __shared__ uint32_t hist[33], off[33];
+    const int tid = threadIdx.x;
+    if (tid < 33) hist[tid] = 0;
+    __syncthreads();
+    for (int t = tid; t < T; t += blockDim.x) {
+        const uint2 r = ranges[t];
+        const uint32_t len = r.y - r.x;
+        atomicAdd(&hist[len ? 32 - __clz(len) : 0], 1u);
+    }
+    __syncthreads();
+    if (tid == 0) {
+        uint32_t run = 0;
+        for (int b = 32; b >= 0; --b) {
+            off[b] = run;
+            run += hist[b];
+        }
+    }
+    __syncthreads();
+    for (int t = tid; t < T; t += blockDim.x) {
+        const uint2 r = ranges[t];
+        const uint32_t len = r.y - r.x;
+        order[atomicAdd(&off[len ? 32 - __clz(len) : 0], 1u)] = (uint32_t)t;
+    }
 }
 
 }  // namespace
@@ -269,13 +304,15 @@ void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_id
 // (keys_out, vals_out).  keys_in/vals_in are not modified.
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_tmp, uint32_t* vals_tmp,
                        uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits, uint32_t* hist,
-                       uint32_t* parts, hipStream_t st) {
+                       uint32_t* parts, hipStream_t st, const uint32_t* vals2_in, uint32_t* vals2_tmp,
+                       uint32_t* vals2_out) {
     if (n == 0) return;
     if (key_bits < 1) key_bits = 1;
     const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
     const size_t nb = sort_blocks(n);
     const uint32_t* kin = keys_in;
     const uint32_t* vin = vals_in;
+    const uint32_t* v2in = vals2_in;
     for (int p = 0; p < passes; ++p) {
         const int shift = p * RADIX_BITS;
         const int bits = key_bits - shift < RADIX_BITS ? key_bits - shift : RADIX_BITS;
@@ -283,14 +320,21 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
         const bool to_out = ((passes - 1 - p) % 2) == 0;
         uint32_t* kout = to_out ? keys_out : keys_tmp;
         uint32_t* vout = to_out ? vals_out : vals_tmp;
+        uint32_t* v2out = vals2_in ? (to_out ? vals2_out : vals2_tmp) : nullptr;
         hipLaunchKernelGGL(k_radix_upsweep, dim3(nb), dim3(SORT_THREADS), 0, st, kin, n, shift,
                            (1u << bits) - 1u, hist);
         scan_exclusive_inplace(hist, (size_t)RADIX * nb, parts, st);
         hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, st, kin, vin, kout, vout, n, shift,
-                           bits, hist);
+                           bits, hist, v2in, v2out);
         kin = kout;
         vin = vout;
+        v2in = v2out;
     }
+}
+
+void launch_tile_order(const uint2* ranges, int T, uint32_t* order, hipStream_t st) {
+    if (T == 0) return;
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ranges, T, order);
 }
 
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
@@ -301,11 +345,9 @@ void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, con
                        gx, tkeys, slot_gid, goff);
 }
 
-void launch_finalize(size_t I, const uint32_t* tkeys, const uint32_t* slot_vals, const uint32_t* slot_gid,
-                     uint32_t* point_list, uint2* ranges, hipStream_t st) {
+void launch_finalize(size_t I, const uint32_t* tkeys, uint2* ranges, hipStream_t st) {
     if (I == 0) return;
-    hipLaunchKernelGGL(k_finalize, dim3(cdiv(I, 256)), dim3(256), 0, st, I, tkeys, slot_vals, slot_gid,
-                       point_list, ranges);
+    hipLaunchKernelGGL(k_finalize, dim3(cdiv(I, 256)), dim3(256), 0, st, I, tkeys, ranges);
 }
 
 }  // namespace gsr

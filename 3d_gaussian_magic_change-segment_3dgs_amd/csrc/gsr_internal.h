@@ -58,7 +58,7 @@ inline GeomLayout geom_layout(size_t P) {
 
 // ---- binning buffer (reference BinningState, rasterizer_impl.cu:181-194) ----
 struct BinLayout {
-    size_t tkeys, tkeys_alt, vals_alt, slot_vals, slot_gid, point_list, hist, parts, bytes;
+    size_t tkeys, tkeys_alt, vals_alt, slot_vals, slot_gid, gid_alt, point_list, hist, parts, bytes;
 };
 inline BinLayout bin_layout(size_t I) {
     BinLayout L{};
@@ -69,6 +69,7 @@ inline BinLayout bin_layout(size_t I) {
     L.vals_alt = take(I * 4);
     L.slot_vals = take(I * 4);
     L.slot_gid = take(I * 4);
+    L.gid_alt = take(I * 4);
     L.point_list = take(I * 4);
     size_t hl = hist_len(I);
     L.hist = take(hl * 4);
@@ -79,7 +80,7 @@ inline BinLayout bin_layout(size_t I) {
 
 // ---- image buffer (reference ImageState, rasterizer_impl.cu:173-179) ----
 struct ImgLayout {
-    size_t ranges, n_contrib, bytes;
+    size_t ranges, n_contrib, order, bytes;
     int gx, gy;
 };
 inline ImgLayout img_layout(int W, int H) {
@@ -91,6 +92,7 @@ inline ImgLayout img_layout(int W, int H) {
     auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes); return r; };
     L.ranges = take(T * 8);
     L.n_contrib = take(T * TILE_PIX * 4);  // tile-major: [tile][local pixel]
+    L.order = take(T * 4);                 // heavy-first tile schedule
     L.bytes = o + ALIGN;
     return L;
 }
@@ -112,19 +114,22 @@ void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const
 // binning.hip
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL = identity*/, uint32_t* keys_tmp,
                        uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,
-                       uint32_t* hist, uint32_t* parts, hipStream_t st);
+                       uint32_t* hist, uint32_t* parts, hipStream_t st, const uint32_t* vals2_in = nullptr,
+                       uint32_t* vals2_tmp = nullptr, uint32_t* vals2_out = nullptr);
+void launch_tile_order(const uint2* ranges, int T, uint32_t* order, hipStream_t st);
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
                                   uint32_t* parts, hipStream_t st);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, int gx, uint32_t* tkeys, uint32_t* slot_gid, uint32_t* goff,
                       hipStream_t st);
-void launch_finalize(size_t I, const uint32_t* tkeys, const uint32_t* slot_vals, const uint32_t* slot_gid,
-                     uint32_t* point_list, uint2* ranges, hipStream_t st);
+void launch_finalize(size_t I, const uint32_t* tkeys, uint2* ranges, hipStream_t st);
 // render.hip
-void launch_render_forward(int W, int H, int gx, int gy, const uint2* ranges, const uint32_t* point_list,
+void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
+                           const uint32_t* point_list,
                            const float4* rec, const float* bg, float* out_color, float* out_depth,
                            float* out_alpha, float* out_segment, uint32_t* n_contrib, hipStream_t st);
-void launch_render_backward(int W, int H, int gx, int gy, const uint2* ranges, const uint32_t* point_list,
+void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
+                            const uint32_t* point_list,
                             const uint32_t* slot_vals, const float4* rec, const float* bg, const float* alpha,
                             const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_dsegment,
                             const float* dL_ddepth, const float* dL_dalpha, float* contrib, hipStream_t st);

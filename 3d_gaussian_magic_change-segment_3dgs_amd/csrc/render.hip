@@ -79,7 +79,24 @@ __device__ __forceinline__ float power_floor(float opacity) {
     return -__logf(255.0f * opacity) - POWER_GUARD;
 }
 
-__global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const uint2* __restrict__ ranges,
+// Batch fetch: lane l loads the 48 B of instance (first + l) of the tile list.
+struct Batch {
+    float4 a, b, c;
+};
+__device__ __forceinline__ Batch fetch_batch(const float4* __restrict__ rec, uint32_t g, bool valid) {
+    Batch r;
+    r.a = r.b = r.c = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (valid) {
+        const float4* R = rec + (size_t)g * REC_F4;
+        r.a = R[0];
+        r.b = R[1];
+        r.c = R[2];
+    }
+    return r;
+}
+
+__global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const uint32_t* __restrict__ order,
+                                                   const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ point_list,
                                                    const float4* __restrict__ rec, const float* __restrict__ bg,
                                                    float* __restrict__ out_color, float* __restrict__ out_depth,
@@ -91,7 +108,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     // rounded exactly as the reference writes them (no contraction); only the
     // colour/depth/segment sums, which nothing amplifies, use explicit FMAs.
 #pragma clang fp contract(off)
-    const int tile = blockIdx.x;
+    const int tile = (int)order[blockIdx.x];
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
     const int px = tx * BX + (lane & 15);
@@ -114,19 +131,20 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
 
+    // Two-stage software pipeline over batches of 64 instances: while batch b is
+    // blended, the records of batch b+1 and the ids of batch b+2 are in flight
+    // (the id -> record dependency would otherwise stall every batch start).
+    uint32_t g_next = lane < n ? point_list[range.x + lane] : 0u;
+    Batch cur = fetch_batch(rec, g_next, lane < n);
+    g_next = 64 + lane < n ? point_list[range.x + 64 + lane] : 0u;
     for (int base = 0; base < n; base += 64) {
         if (!__any(T[0] > 0.f || T[1] > 0.f || T[2] > 0.f || T[3] > 0.f)) break;
         const int cnt = min(64, n - base);
-        float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra, rc = ra;
-        float pmin = 0.f;
-        if (lane < cnt) {
-            const uint32_t g = point_list[range.x + base + lane];
-            const float4* R = rec + (size_t)g * REC_F4;
-            ra = R[0];
-            rb = R[1];
-            rc = R[2];
-            pmin = power_floor(rb.y);
-        }
+        const Batch nxt = fetch_batch(rec, g_next, base + 64 + lane < n);
+        g_next = base + 128 + lane < n ? point_list[range.x + base + 128 + lane] : 0u;
+        const float4 ra = cur.a, rb = cur.b, rc = cur.c;
+        const float pmin = lane < cnt ? power_floor(rb.y) : 0.f;
+        cur = nxt;
         for (int j = 0; j < cnt; ++j) {
             const float gx_ = bcast(ra.x, j), gy_ = bcast(ra.y, j);
             const float ca = bcast(ra.z, j), cb = bcast(ra.w, j), cc = bcast(rb.x, j), pm = bcast(pmin, j);
@@ -247,7 +265,8 @@ __device__ __forceinline__ float fdiv(float num, float den) {
     return __builtin_fmaf(e, r, q);
 }
 
-__global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const uint2* __restrict__ ranges,
+__global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const uint32_t* __restrict__ order,
+                                                   const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ point_list,
                                                    const uint32_t* __restrict__ slot_vals,
                                                    const float4* __restrict__ rec, const float* __restrict__ bg,
@@ -259,7 +278,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
                                                    const float* __restrict__ dL_dalphas,
                                                    float* __restrict__ contrib) {
 #pragma clang fp contract(off)
-    const int tile = blockIdx.x;
+    const int tile = (int)order[blockIdx.x];
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
     const int px = tx * BX + (lane & 15);
@@ -318,21 +337,29 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
         dst[2] = z;
     }
 
-    for (int top = (int)maxlast; top > 0; top -= 64) {
+    // Same two-stage batch pipeline as the forward, walking the list back to front:
+    // lane l of the batch with upper end `top` owns position top-1-l.
+    const int top0 = (int)maxlast;
+    bool v_next = lane < top0;
+    uint32_t g_next = v_next ? point_list[range.x + (uint32_t)(top0 - 1 - lane)] : 0u;
+    uint32_t u_next = v_next ? slot_vals[range.x + (uint32_t)(top0 - 1 - lane)] : 0u;
+    Batch cur = fetch_batch(rec, g_next, v_next);
+    uint32_t u_cur = u_next;
+    v_next = 64 + lane < top0;
+    g_next = v_next ? point_list[range.x + (uint32_t)(top0 - 65 - lane)] : 0u;
+    u_next = v_next ? slot_vals[range.x + (uint32_t)(top0 - 65 - lane)] : 0u;
+    for (int top = top0; top > 0; top -= 64) {
         const int cnt = min(64, top);
-        float4 ra = make_float4(0.f, 0.f, 0.f, 0.f), rb = ra, rc = ra;
-        uint32_t uslot = 0;
-        float pmin = 0.f;
-        if (lane < cnt) {
-            const uint32_t kidx = range.x + (uint32_t)(top - 1 - lane);
-            const uint32_t g = point_list[kidx];
-            uslot = slot_vals[kidx];
-            const float4* R = rec + (size_t)g * REC_F4;
-            ra = R[0];
-            rb = R[1];
-            rc = R[2];
-            pmin = power_floor(rb.y);
-        }
+        const Batch nxt = fetch_batch(rec, g_next, v_next);
+        const uint32_t u_nxt = u_next;
+        v_next = 128 + lane < top;
+        g_next = v_next ? point_list[range.x + (uint32_t)(top - 129 - lane)] : 0u;
+        u_next = v_next ? slot_vals[range.x + (uint32_t)(top - 129 - lane)] : 0u;
+        const float4 ra = cur.a, rb = cur.b, rc = cur.c;
+        const uint32_t uslot = u_cur;
+        const float pmin = lane < cnt ? power_floor(rb.y) : 0.f;
+        cur = nxt;
+        u_cur = u_nxt;
         for (int j = 0; j < cnt; ++j) {
             const uint32_t p = (uint32_t)(top - 1 - j);
             const uint32_t u = bcast_u(uslot, j);
@@ -428,23 +455,25 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
 
 }  // namespace
 
-void launch_render_forward(int W, int H, int gx, int gy, const uint2* ranges, const uint32_t* point_list,
-                           const float4* rec, const float* bg, float* out_color, float* out_depth, float* out_alpha,
-                           float* out_segment, uint32_t* n_contrib, hipStream_t st) {
+void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
+                           const uint32_t* point_list, const float4* rec, const float* bg, float* out_color,
+                           float* out_depth, float* out_alpha, float* out_segment, uint32_t* n_contrib,
+                           hipStream_t st) {
     const int T = gx * gy;
     if (T == 0) return;
-    hipLaunchKernelGGL(k_render_fwd, dim3(T), dim3(64), 0, st, W, H, gx, ranges, point_list, rec, bg, out_color,
-                       out_depth, out_alpha, out_segment, n_contrib);
+    hipLaunchKernelGGL(k_render_fwd, dim3(T), dim3(64), 0, st, W, H, gx, order, ranges, point_list, rec, bg,
+                       out_color, out_depth, out_alpha, out_segment, n_contrib);
 }
 
-void launch_render_backward(int W, int H, int gx, int gy, const uint2* ranges, const uint32_t* point_list,
-                            const uint32_t* slot_vals, const float4* rec, const float* bg, const float* alpha,
-                            const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_dsegment,
-                            const float* dL_ddepth, const float* dL_dalpha, float* contrib, hipStream_t st) {
+void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
+                            const uint32_t* point_list, const uint32_t* slot_vals, const float4* rec,
+                            const float* bg, const float* alpha, const uint32_t* n_contrib, const float* dL_dcolor,
+                            const float* dL_dsegment, const float* dL_ddepth, const float* dL_dalpha, float* contrib,
+                            hipStream_t st) {
     const int T = gx * gy;
     if (T == 0) return;
-    hipLaunchKernelGGL(k_render_bwd, dim3(T), dim3(64), 0, st, W, H, gx, ranges, point_list, slot_vals, rec, bg,
-                       alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib);
+    hipLaunchKernelGGL(k_render_bwd, dim3(T), dim3(64), 0, st, W, H, gx, order, ranges, point_list, slot_vals, rec,
+                       bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib);
 }
 
 }  // namespace gsr

@@ -4,8 +4,11 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out
-timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; echo "pytest rc=$?" >> gpurun_out/pytest_gpu.log
-tail -5 gpurun_out/pytest_gpu.log
+timeout -k 10 600 python -m pytest tests -x -q -m gpu > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+echo "pytest rc=$rc" >> gpurun_out/pytest_gpu.log
+tail -25 gpurun_out/pytest_gpu.log
+# A crash, abort or time limit ends the session; an ordinary test failure does not.
+if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo smoke failed; cat gpurun_out/smoke.log; exit 1; }
 cat gpurun_out/smoke.log
 timeout -k 10 400 python bench.py --stages > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo bench failed; cat gpurun_out/bench.err; exit 1; }
