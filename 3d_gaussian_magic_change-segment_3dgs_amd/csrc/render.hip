@@ -57,6 +57,32 @@ __device__ __forceinline__ float gsr_expf(float x) {
 #define GSR_EXP(x) gsr_expf(x)
 #endif
 
+#ifdef GSR_STATS
+// Instrumented build (tools/render_stats.py): wave-uniform loop counters, 16 per
+// kernel (fwd at 0, bwd at 16): 0 visited, 1 near-skip, 2 prefiltered out, 3 full,
+// 4 ok pixels, 5 batches, 6 zero-tail (bwd), 7 instances, 8 strips processed.
+__device__ unsigned long long g_gsr_stats[32];
+extern "C" __attribute__((visibility("default"))) int gsr_stats_read(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gsr_stats), sizeof(g_gsr_stats)) != hipSuccess) return -1;
+    if (reset) {
+        unsigned long long z[32] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(g_gsr_stats), z, sizeof(z)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#define STAT_DECL unsigned long long st_[16] = {};
+#define STAT(i, v) (st_[i] += (v))
+#define STAT_FLUSH(off)                                                          \
+    if (threadIdx.x == 0)                                                        \
+        for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_gsr_stats[(off) + i_], st_[i_]);
+#define POPC(a) __popcll(__ballot(a))
+#else
+#define STAT_DECL
+#define STAT(i, v)
+#define STAT_FLUSH(off)
+#define POPC(a) 0
+#endif
+
 namespace gsr {
 namespace {
 
@@ -95,6 +121,30 @@ __device__ __forceinline__ Batch fetch_batch(const float4* __restrict__ rec, uin
     return r;
 }
 
+// Lane-parallel batch prefilter: can ANY pixel centre of the tile rectangle
+// [x0,x1] x [y0,y1] reach power >= pm for the Gaussian (x, y, conic a, b, c)?
+// power = -q/2 with q(u,v) = a u^2 + 2 b u v + c v^2 convex (a, c, det > 0), so the
+// minimum of q over the rectangle is 0 when the centre lies inside, otherwise on
+// one of the four edges, where it is a 1-D quadratic minimised in closed form.
+// The test is conservative: the margin covers fp32 rounding of the terms, and a
+// non-convex conic always passes.  Skipping a Gaussian here only avoids work that
+// the exact per-pixel tests of the blend loop would have rejected.
+__device__ __forceinline__ bool tile_hit(float x, float y, float a, float b, float c, float pm, float x0,
+                                         float x1, float y0, float y1) {
+    if (!(a > 0.f && c > 0.f && a * c > b * b)) return true;
+    const float ul = x0 - x, uh = x1 - x, vl = y0 - y, vh = y1 - y;
+    const float ra = __builtin_amdgcn_rcpf(a), rc = __builtin_amdgcn_rcpf(c);
+    auto q = [&](float u, float v) { return (a * u + 2.f * b * v) * u + c * v * v; };
+    const float v_l = fminf(fmaxf(-b * ul * rc, vl), vh), v_h = fminf(fmaxf(-b * uh * rc, vl), vh);
+    const float u_l = fminf(fmaxf(-b * vl * ra, ul), uh), u_h = fminf(fmaxf(-b * vh * ra, ul), uh);
+    float qmin = fminf(fminf(q(ul, v_l), q(uh, v_h)), fminf(q(u_l, vl), q(u_h, vh)));
+    const bool inside = ul <= 0.f && uh >= 0.f && vl <= 0.f && vh >= 0.f;
+    qmin = inside ? 0.f : qmin;
+    const float U = fmaxf(-ul, uh), V = fmaxf(-vl, vh);
+    const float margin = 1e-2f + 1e-5f * (a * U * U + 2.f * fabsf(b) * U * V + c * V * V);
+    return qmin <= -2.f * pm + margin;
+}
+
 __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const uint32_t* __restrict__ order,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ point_list,
@@ -130,6 +180,10 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     }
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
+    STAT_DECL
+    STAT(7, n);
+    const float x0 = (float)(tx * BX), y0 = (float)(ty * BY);
+    const float x1 = (float)min(tx * BX + BX - 1, W - 1), y1 = (float)min(ty * BY + BY - 1, H - 1);
 
     // Two-stage software pipeline over batches of 64 instances: while batch b is
     // blended, the records of batch b+1 and the ids of batch b+2 are in flight
@@ -138,47 +192,54 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     Batch cur = fetch_batch(rec, g_next, lane < n);
     g_next = 64 + lane < n ? point_list[range.x + 64 + lane] : 0u;
     for (int base = 0; base < n; base += 64) {
-        if (!__any(T[0] > 0.f || T[1] > 0.f || T[2] > 0.f || T[3] > 0.f)) break;
+        if (!__any((T[0] > 0.f) | (T[1] > 0.f) | (T[2] > 0.f) | (T[3] > 0.f))) break;
         const int cnt = min(64, n - base);
+        STAT(5, 1);
         const Batch nxt = fetch_batch(rec, g_next, base + 64 + lane < n);
         g_next = base + 128 + lane < n ? point_list[range.x + base + 128 + lane] : 0u;
         const float4 ra = cur.a, rb = cur.b, rc = cur.c;
-        const float pmin = lane < cnt ? power_floor(rb.y) : 0.f;
         cur = nxt;
-        for (int j = 0; j < cnt; ++j) {
+        const float pmin = power_floor(rb.y);
+        uint64_t todo = __ballot(lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1));
+        STAT(2, cnt - __popcll(todo));
+        while (todo) {
+            const int j = (int)__builtin_ctzll(todo);
+            todo &= todo - 1;
             const float gx_ = bcast(ra.x, j), gy_ = bcast(ra.y, j);
             const float ca = bcast(ra.z, j), cb = bcast(ra.w, j), cc = bcast(rb.x, j), pm = bcast(pmin, j);
             float power[4];
-            bool near = false;
+            bool near[4];
+            const float dx = gx_ - pfx;
+            const float adxdx = ca * dx * dx, bdx = cb * dx;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float dx = gx_ - pfx, dy = gy_ - pfy[k];
-                power[k] = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
-                near = near || (power[k] >= pm && T[k] > 0.f);
+                const float dy = gy_ - pfy[k];
+                power[k] = -0.5f * (adxdx + cc * dy * dy) - bdx * dy;
+                near[k] = (power[k] >= pm) & (T[k] > 0.f);
             }
-            if (!__any(near)) continue;
-            const float op = bcast(rb.y, j);
-            bool ok[4];
-            float alpha[4];
-            bool any_ok = false;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                alpha[k] = fminf(0.99f, op * GSR_EXP(power[k]));
-                const bool o = power[k] <= 0.0f && alpha[k] >= ALPHA_MIN;
-                const float test_T = T[k] * (1.f - alpha[k]);
-                const bool term = o && T[k] > 0.f && test_T < T_MIN;
-                Tend[k] = term ? T[k] : Tend[k];
-                ok[k] = o && test_T >= T_MIN;
-                T[k] = term ? 0.f : T[k];
-                any_ok = any_ok || ok[k];
+            STAT(0, 1);
+            if (!__any(near[0] | near[1] | near[2] | near[3])) {
+                STAT(1, 1);
+                continue;
             }
-            if (!__any(any_ok)) continue;
-            const float dep = bcast(rb.z, j), s0 = bcast(rb.w, j);
+            STAT(3, 1);
+            const float op = bcast(rb.y, j), dep = bcast(rb.z, j), s0 = bcast(rb.w, j);
             const float cr = bcast(rc.x, j), cg = bcast(rc.y, j), cbl = bcast(rc.z, j), s1 = bcast(rc.w, j);
             const uint32_t contributor = (uint32_t)(base + j + 1);
+            // Strip k (rows 4k..4k+3 of the tile) is blended only if one of its pixels
+            // can pass; the exact reference tests below decide per pixel.
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float aT = (ok[k] ? alpha[k] : 0.f) * T[k];
+                if (!__any(near[k])) continue;
+                STAT(8, 1);
+                const float alpha = fminf(0.99f, op * GSR_EXP(power[k]));
+                const bool o = (power[k] <= 0.0f) & (alpha >= ALPHA_MIN);
+                const float test_T = T[k] * (1.f - alpha);
+                const bool term = o & (T[k] > 0.f) & (test_T < T_MIN);
+                const bool ok = o & (test_T >= T_MIN);
+                STAT(4, POPC(ok));
+                Tend[k] = term ? T[k] : Tend[k];
+                const float aT = (ok ? alpha : 0.f) * T[k];
                 C0[k] = __builtin_fmaf(cr, aT, C0[k]);
                 C1[k] = __builtin_fmaf(cg, aT, C1[k]);
                 C2[k] = __builtin_fmaf(cbl, aT, C2[k]);
@@ -186,11 +247,12 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
                 Dp[k] = __builtin_fmaf(dep, aT, Dp[k]);
                 S0[k] = __builtin_fmaf(s0, aT, S0[k]);
                 S1[k] = __builtin_fmaf(s1, aT, S1[k]);
-                T[k] = ok[k] ? T[k] * (1.f - alpha[k]) : T[k];
-                last[k] = ok[k] ? contributor : last[k];
+                T[k] = ok ? test_T : (term ? 0.f : T[k]);
+                last[k] = ok ? contributor : last[k];
             }
         }
     }
+    STAT_FLUSH(0)
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
     const size_t HW = (size_t)H * W;
 #pragma unroll
@@ -327,7 +389,12 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
     const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
+    const float x0 = (float)(tx * BX), y0 = (float)(ty * BY);
+    const float x1 = (float)min(tx * BX + BX - 1, W - 1), y1 = (float)min(ty * BY + BY - 1, H - 1);
 
+    STAT_DECL
+    STAT(7, n);
+    STAT(6, n > (int)maxlast ? n - (int)maxlast : 0);
     // Instances behind every pixel's last contributor carry no gradient.
     for (int p = (int)maxlast + lane; p < n; p += 64) {
         float4* dst = reinterpret_cast<float4*>(contrib + (size_t)slot_vals[range.x + p] * 12);
@@ -350,6 +417,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
     u_next = v_next ? slot_vals[range.x + (uint32_t)(top0 - 65 - lane)] : 0u;
     for (int top = top0; top > 0; top -= 64) {
         const int cnt = min(64, top);
+        STAT(5, 1);
         const Batch nxt = fetch_batch(rec, g_next, v_next);
         const uint32_t u_nxt = u_next;
         v_next = 128 + lane < top;
@@ -357,53 +425,59 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
         u_next = v_next ? slot_vals[range.x + (uint32_t)(top - 129 - lane)] : 0u;
         const float4 ra = cur.a, rb = cur.b, rc = cur.c;
         const uint32_t uslot = u_cur;
-        const float pmin = lane < cnt ? power_floor(rb.y) : 0.f;
         cur = nxt;
         u_cur = u_nxt;
-        for (int j = 0; j < cnt; ++j) {
+        const float pmin = power_floor(rb.y);
+        const bool hit = lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1);
+        if (lane < cnt && !hit) {  // no pixel of the tile can be reached: zero record, in parallel
+            float4* d4 = reinterpret_cast<float4*>(contrib + (size_t)uslot * 12);
+            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+            d4[0] = z;
+            d4[1] = z;
+            d4[2] = z;
+        }
+        uint64_t todo = __ballot(hit);
+        STAT(2, cnt - __popcll(todo));
+        while (todo) {
+            const int j = (int)__builtin_ctzll(todo);
+            todo &= todo - 1;
             const uint32_t p = (uint32_t)(top - 1 - j);
             const uint32_t u = bcast_u(uslot, j);
             float* dst = contrib + (size_t)u * 12;
             const float gx_ = bcast(ra.x, j), gy_ = bcast(ra.y, j);
             const float ca = bcast(ra.z, j), cb = bcast(ra.w, j), cc = bcast(rb.x, j), pm = bcast(pmin, j);
-            float power[4], dxs[4], dys[4];
-            bool near = false;
+            float power[4], dys[4];
+            bool near[4];
+            const float dx = gx_ - pfx;
+            const float adxdx = ca * dx * dx, bdx = cb * dx;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float dx = gx_ - pfx, dy = gy_ - pfy[k];
-                dxs[k] = dx;
+                const float dy = gy_ - pfy[k];
                 dys[k] = dy;
-                power[k] = -0.5f * (ca * dx * dx + cc * dy * dy) - cb * dx * dy;
-                near = near || (p < lastc[k] && power[k] >= pm);
+                power[k] = -0.5f * (adxdx + cc * dy * dy) - bdx * dy;
+                near[k] = (p < lastc[k]) & (power[k] >= pm);
             }
-            if (!__any(near)) {
+            STAT(0, 1);
+            if (!__any(near[0] | near[1] | near[2] | near[3])) {
+                STAT(1, 1);
                 if (lane < 12) dst[lane] = 0.f;
                 continue;
             }
-            const float op = bcast(rb.y, j);
-            bool ok[4];
-            float G[4], alpha[4];
-            bool any_ok = false;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                G[k] = GSR_EXP(power[k]);
-                alpha[k] = fminf(0.99f, op * G[k]);
-                ok[k] = p < lastc[k] && power[k] <= 0.0f && alpha[k] >= ALPHA_MIN;
-                any_ok = any_ok || ok[k];
-            }
-            if (!__any(any_ok)) {
-                if (lane < 12) dst[lane] = 0.f;
-                continue;
-            }
-            const float dep = bcast(rb.z, j), s0 = bcast(rb.w, j);
+            STAT(3, 1);
+            const float op = bcast(rb.y, j), dep = bcast(rb.z, j), s0 = bcast(rb.w, j);
             const float c0 = bcast(rc.x, j), c1 = bcast(rc.y, j), c2 = bcast(rc.z, j), s1 = bcast(rc.w, j);
             float acc[12];
 #pragma unroll
             for (int i = 0; i < 12; ++i) acc[i] = 0.f;
+            // Strip k (rows 4k..4k+3) is replayed only if one of its pixels can pass.
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const bool o = ok[k];
-                const float a = alpha[k];
+                if (!__any(near[k])) continue;
+                STAT(8, 1);
+                const float G = GSR_EXP(power[k]);
+                const float a = fminf(0.99f, op * G);
+                const bool o = (p < lastc[k]) & (power[k] <= 0.0f) & (a >= ALPHA_MIN);
+                STAT(4, POPC(o));
                 const float one_m = 1.f - a;
                 const float Tn = fdiv(T[k], one_m);
                 const float dch = a * Tn;
@@ -420,7 +494,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
                 const float dopa_m = o ? dopa : 0.f;
                 const float dch_m = o ? dch : 0.f;
                 const float dL_dG = op * dopa_m;
-                const float gdx = G[k] * dxs[k], gdy = G[k] * dys[k];
+                const float gdx = G * dx, gdy = G * dys[k];
                 const float dG_ddelx = -gdx * ca - gdy * cb;
                 const float dG_ddely = -gdy * cc - gdx * cb;
                 acc[0] += dch_m * dp0[k];
@@ -431,10 +505,10 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
                 acc[5] += dch_m * dd[k];
                 acc[6] += dL_dG * dG_ddelx * ddelx_dx;
                 acc[7] += dL_dG * dG_ddely * ddely_dy;
-                acc[8] += -0.5f * gdx * dxs[k] * dL_dG;
+                acc[8] += -0.5f * gdx * dx * dL_dG;
                 acc[9] += -0.5f * gdx * dys[k] * dL_dG;
                 acc[10] += -0.5f * gdy * dys[k] * dL_dG;
-                acc[11] += G[k] * dopa_m;
+                acc[11] += G * dopa_m;
                 // fold this contributor into the accumulators seen by the next one (front side)
                 ar0[k] = o ? a * c0 + one_m * ar0[k] : ar0[k];
                 ar1[k] = o ? a * c1 + one_m * ar1[k] : ar1[k];
@@ -451,6 +525,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
             if (valid) dst[vidx] = r;
         }
     }
+    STAT_FLUSH(16)
 }
 
 }  // namespace
