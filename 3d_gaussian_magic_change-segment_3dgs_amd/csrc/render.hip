@@ -349,13 +349,17 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
     const size_t HW = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
 
-    // Per-pixel replay state.  The reference keeps (last_alpha, last_color, ...) and
-    // folds them into accum_rec at the NEXT contributor (backward.cu:567,583,598,604);
-    // here the same expression a*c + (1-a)*accum is evaluated right after the
-    // contributor that owns (a, c) -- identical operands and operations, one step
-    // earlier -- so no last_* registers are needed.
+    // Per-pixel replay state.  The reference keeps seven per-channel accum_rec
+    // registers (colour, segment, depth, alpha) plus last_alpha/last_colour and folds
+    // them in at the NEXT contributor (backward.cu:567-606).  Here each pixel keeps
+    // only their projection on its upstream gradient, Dk = sum_ch accum_rec[ch] *
+    // dL_dch (alpha channel: colour 1), folded right after the contributor that owns
+    // (a, c): Dk' = a * cdot + (1 - a) * Dk with cdot = sum_ch c[ch] * dL_dch, and the
+    // reference's sum_ch (c[ch] - accum_rec[ch]) * dL_dch is cdot - Dk.  Equal in exact
+    // arithmetic; the fp32 rounding differs from the per-channel form at the 1e-7
+    // level (tests/test_gpu_parity.py tolerances), and 24 registers per lane are freed.
     float pfy[4], T[4], Tfin[4], dp0[4], dp1[4], dp2[4], ds0[4], ds1[4], dd[4], da[4], bgdot[4];
-    float ar0[4], ar1[4], ar2[4], as0[4], as1[4], ad[4], aa[4];
+    float Dk[4];
     uint32_t lastc[4];
     uint32_t maxlast = 0;
 #pragma unroll
@@ -379,7 +383,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
         bgd += bg1 * dp1[k];
         bgd += bg2 * dp2[k];
         bgdot[k] = bgd;
-        ar0[k] = ar1[k] = ar2[k] = as0[k] = as1[k] = ad[k] = aa[k] = 0.f;
+        Dk[k] = 0.f;
         maxlast = max(maxlast, lastc[k]);
     }
 #pragma unroll
@@ -481,14 +485,14 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
                 const float one_m = 1.f - a;
                 const float Tn = fdiv(T[k], one_m);
                 const float dch = a * Tn;
-                float dopa = 0.f;
-                dopa += (c0 - ar0[k]) * dp0[k];
-                dopa += (c1 - ar1[k]) * dp1[k];
-                dopa += (c2 - ar2[k]) * dp2[k];
-                dopa += (s0 - as0[k]) * ds0[k];
-                dopa += (s1 - as1[k]) * ds1[k];
-                dopa += (dep - ad[k]) * dd[k];
-                dopa += (1.f - aa[k]) * da[k];
+                float cdot = c0 * dp0[k];
+                cdot = __builtin_fmaf(c1, dp1[k], cdot);
+                cdot = __builtin_fmaf(c2, dp2[k], cdot);
+                cdot = __builtin_fmaf(s0, ds0[k], cdot);
+                cdot = __builtin_fmaf(s1, ds1[k], cdot);
+                cdot = __builtin_fmaf(dep, dd[k], cdot);
+                cdot += da[k];
+                float dopa = cdot - Dk[k];
                 dopa *= Tn;
                 if (use_bg) dopa += (-Tfin[k] * __builtin_amdgcn_rcpf(one_m)) * bgdot[k];
                 const float dopa_m = o ? dopa : 0.f;
@@ -510,13 +514,7 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
                 acc[10] += -0.5f * gdy * dys[k] * dL_dG;
                 acc[11] += G * dopa_m;
                 // fold this contributor into the accumulators seen by the next one (front side)
-                ar0[k] = o ? a * c0 + one_m * ar0[k] : ar0[k];
-                ar1[k] = o ? a * c1 + one_m * ar1[k] : ar1[k];
-                ar2[k] = o ? a * c2 + one_m * ar2[k] : ar2[k];
-                as0[k] = o ? a * s0 + one_m * as0[k] : as0[k];
-                as1[k] = o ? a * s1 + one_m * as1[k] : as1[k];
-                ad[k] = o ? a * dep + one_m * ad[k] : ad[k];
-                aa[k] = o ? a + one_m * aa[k] : aa[k];
+                Dk[k] = o ? __builtin_fmaf(a, cdot, one_m * Dk[k]) : Dk[k];
                 T[k] = o ? Tn : T[k];
             }
             int vidx;
