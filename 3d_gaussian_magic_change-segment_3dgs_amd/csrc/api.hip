@@ -272,7 +272,7 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
     {
         StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);
         launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
-                                 at<uint8_t>(g, GL.clamped), contrib, *grads, st);
+                                 at<uint8_t>(g, GL.clamped), contrib, at<float4>(g, GL.rec), *grads, st);
     }
     GSR_STAGE("gaussian backward");
     return 0;

@@ -110,7 +110,7 @@ void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const gsr_grads& g, hipStream_t st);
+                              const float* contrib, const float4* rec, const gsr_grads& g, hipStream_t st);
 // binning.hip
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL = identity*/, uint32_t* keys_tmp,
                        uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,

@@ -268,14 +268,21 @@ __global__ void k_mark_visible(int P, const float* __restrict__ means3D, const f
 // the render backward wrote at the Gaussian's instance slots (replacing the
 // reference's 12 per-pixel atomicAdds, backward.cu:575-636), then runs
 // computeCov2DCUDA (backward.cu:141-274) and preprocessCUDA backward
-// (backward.cu:343-412) on the sums.  Record layout (12 floats):
-//   [dcolor.rgb, dseg0, dseg1, ddepth, dmean2D.x, dmean2D.y, dconic.x, dconic.y, dconic.w, dopacity]
+// (backward.cu:343-412) on the sums.  Record layout (12 floats, render.hip):
+//   [dcolor.rgb, dseg0, dseg1, ddepth, Q, Qx, Qy, Qxx, Qxy, Qyy]
+// with Q* the moments of q = G * dL_dalpha over the Gaussian's pixels.  Since
+// dL_dG = opacity * dL_dalpha and conic/opacity are per-Gaussian constants
+// (backward.cu:612-636):
+//   dopacity  = Q
+//   dmean2D.x = -o (a Qx + b Qy) W/2,   dmean2D.y = -o (c Qy + b Qx) H/2
+//   dconic    = -o/2 (Qxx, Qxy, Qyy)    for conic (a, b, c), opacity o.
 __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_inputs in,
                                                            const int* __restrict__ radii,
                                                            const uint32_t* __restrict__ tiles_touched,
                                                            const uint32_t* __restrict__ goff,
                                                            const uint8_t* __restrict__ clamped,
-                                                           const float* __restrict__ contrib, gsr_grads g) {
+                                                           const float* __restrict__ contrib,
+                                                           const float4* __restrict__ rec, gsr_grads g) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= s.P) return;
     const int M = s.M;
@@ -307,9 +314,13 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
             q[8] += c.x; q[9] += c.y; q[10] += c.z; q[11] += c.w;
         }
     }
-    if (g.dmeans2D) { g.dmeans2D[i3] = q[6]; g.dmeans2D[i3 + 1] = q[7]; g.dmeans2D[i3 + 2] = 0.f; }
+    const float4 r0 = rec[(size_t)idx * REC_F4], r1 = rec[(size_t)idx * REC_F4 + 1];
+    const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
+    const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * s.W);
+    const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * s.H);
+    if (g.dmeans2D) { g.dmeans2D[i3] = dm2x; g.dmeans2D[i3 + 1] = dm2y; g.dmeans2D[i3 + 2] = 0.f; }
     if (g.dcolors) { g.dcolors[i3] = q[0]; g.dcolors[i3 + 1] = q[1]; g.dcolors[i3 + 2] = q[2]; }
-    if (g.dopacity) g.dopacity[idx] = q[11];
+    if (g.dopacity) g.dopacity[idx] = q[6];
     if (g.dsegments) { g.dsegments[2 * (size_t)idx] = q[3]; g.dsegments[2 * (size_t)idx + 1] = q[4]; }
 
     Cam cam;
@@ -330,7 +341,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         scale = ld3(in.scales + i3);
         cov3d_from(scale, s.scale_modifier, quat, c3);  // == the forward's geom.cov3D
     }
-    const float dcx = q[8], dcy = q[9], dcz = q[10];
+    const float dcx = -0.5f * op * q[9], dcy = -0.5f * op * q[10], dcz = -0.5f * op * q[11];
     const EwaTerms e = ewa_terms(mean, focal_x, focal_y, s.tanfovx, s.tanfovy, cam.view);
     const float x_grad_mul = e.txtz < -e.limx || e.txtz > e.limx ? 0 : 1;
     const float y_grad_mul = e.tytz < -e.limy || e.tytz > e.limy ? 0 : 1;
@@ -395,7 +406,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
     const f3 m = mean;
     const float4 m_hom = xform4x4(m, proj);
     const float m_w = 1.0f / (m_hom.w + 0.0000001f);
-    const float d2x = q[6], d2y = q[7];
+    const float d2x = dm2x, d2y = dm2y;
     const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
     const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
     f3 dm;
@@ -553,10 +564,10 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const gsr_grads& g, hipStream_t st) {
+                              const float* contrib, const float4* rec, const gsr_grads& g, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_gaussian_backward, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, radii, tiles_touched,
-                       goff, clamped, contrib, g);
+                       goff, clamped, contrib, rec, g);
 }
 
 }  // namespace gsr

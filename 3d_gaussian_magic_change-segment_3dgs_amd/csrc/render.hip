@@ -20,7 +20,12 @@
 // v_permlane16_swap / DPP (34 VALU ops, no LDS round trips), and 12 lanes
 // store ONE 48-B record per (tile, Gaussian) instance at the instance's slot.
 // The per-Gaussian backward kernel sums a Gaussian's slots in fixed order:
-// deterministic, atomic-free gradients.
+// deterministic, atomic-free gradients.  Record (q = G * dL_dalpha per pixel,
+// d = (dx, dy) = mean2D - pixel):
+//   [sum dch*dL_dcolor.rgb, sum dch*dL_dseg0/1, sum dch*dL_ddepth,
+//    sum q, sum q dx, sum q dy, sum q dx^2, sum q dx dy, sum q dy^2]
+// from which k_gaussian_backward forms dopacity = sum q and the reference's
+// mean2D / conic gradients with the Gaussian's own conic and opacity.
 #include "gsr_internal.h"
 
 // Numerics.  The blend thresholds alpha >= 1/255 and T*(1-alpha) >= 1e-4
@@ -327,7 +332,7 @@ __device__ __forceinline__ float fdiv(float num, float den) {
     return __builtin_fmaf(e, r, q);
 }
 
-__global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const uint32_t* __restrict__ order,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_render_bwd(int W, int H, int gx, const uint32_t* __restrict__ order,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ point_list,
                                                    const uint32_t* __restrict__ slot_vals,
@@ -392,7 +397,6 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
 
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
-    const float ddelx_dx = 0.5f * W, ddely_dy = 0.5f * H;
     const float x0 = (float)(tx * BX), y0 = (float)(ty * BY);
     const float x1 = (float)min(tx * BX + BX - 1, W - 1), y1 = (float)min(ty * BY + BY - 1, H - 1);
 
@@ -497,26 +501,28 @@ __global__ void __launch_bounds__(64) k_render_bwd(int W, int H, int gx, const u
                 if (use_bg) dopa += (-Tfin[k] * __builtin_amdgcn_rcpf(one_m)) * bgdot[k];
                 const float dopa_m = o ? dopa : 0.f;
                 const float dch_m = o ? dch : 0.f;
-                const float dL_dG = op * dopa_m;
-                const float gdx = G * dx, gdy = G * dys[k];
-                const float dG_ddelx = -gdx * ca - gdy * cb;
-                const float dG_ddely = -gdy * cc - gdx * cb;
-                acc[0] += dch_m * dp0[k];
-                acc[1] += dch_m * dp1[k];
-                acc[2] += dch_m * dp2[k];
-                acc[3] += dch_m * ds0[k];
-                acc[4] += dch_m * ds1[k];
-                acc[5] += dch_m * dd[k];
-                acc[6] += dL_dG * dG_ddelx * ddelx_dx;
-                acc[7] += dL_dG * dG_ddely * ddely_dy;
-                acc[8] += -0.5f * gdx * dx * dL_dG;
-                acc[9] += -0.5f * gdx * dys[k] * dL_dG;
-                acc[10] += -0.5f * gdy * dys[k] * dL_dG;
-                acc[11] += G * dopa_m;
+                acc[0] = __builtin_fmaf(dch_m, dp0[k], acc[0]);
+                acc[1] = __builtin_fmaf(dch_m, dp1[k], acc[1]);
+                acc[2] = __builtin_fmaf(dch_m, dp2[k], acc[2]);
+                acc[3] = __builtin_fmaf(dch_m, ds0[k], acc[3]);
+                acc[4] = __builtin_fmaf(dch_m, ds1[k], acc[4]);
+                acc[5] = __builtin_fmaf(dch_m, dd[k], acc[5]);
+                // q = G * dL_dalpha: the opacity gradient term (backward.cu:636); the
+                // mean2D / conic terms (backward.cu:612-631) are op * q times a
+                // polynomial in (dx, dy) with per-Gaussian coefficients, so only the
+                // moments of q are summed here (see the record layout above).
+                const float qg = G * dopa_m;
+                const float qdy = qg * dys[k];
+                acc[6] += qg;
+                acc[8] += qdy;
+                acc[11] = __builtin_fmaf(qdy, dys[k], acc[11]);
                 // fold this contributor into the accumulators seen by the next one (front side)
                 Dk[k] = o ? __builtin_fmaf(a, cdot, one_m * Dk[k]) : Dk[k];
                 T[k] = o ? Tn : T[k];
             }
+            acc[7] = dx * acc[6];   // sum q dx   (dx is shared by the lane's 4 pixels)
+            acc[9] = dx * acc[7];   // sum q dx^2
+            acc[10] = dx * acc[8];  // sum q dx dy
             int vidx;
             bool valid;
             const float r = wave_reduce12(acc, lane, vidx, valid);
