@@ -265,14 +265,15 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
             launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order), at<uint2>(im, IL.ranges),
                                    at<uint32_t>(b, BL.point_list), at<uint32_t>(b, BL.slot_vals),
                                    at<float4>(g, GL.rec), s->bg, alpha, at<uint32_t>(im, IL.n_contrib), dL_dcolor,
-                                   dL_dsegment, dL_ddepth, dL_dalpha, contrib, st);
+                                   dL_dsegment, dL_ddepth, dL_dalpha, contrib, at<uint64_t>(im, IL.cut), st);
         }
         GSR_STAGE("render backward");
     }
     {
         StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);
         launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
-                                 at<uint8_t>(g, GL.clamped), contrib, at<float4>(g, GL.rec), *grads, st);
+                                 at<uint8_t>(g, GL.clamped), contrib, at<float4>(g, GL.rec),
+                                 at<ushort4>(g, GL.rect), at<uint64_t>(im, IL.cut), IL.gx, *grads, st);
     }
     GSR_STAGE("gaussian backward");
     return 0;

@@ -282,7 +282,9 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
                                                            const uint32_t* __restrict__ goff,
                                                            const uint8_t* __restrict__ clamped,
                                                            const float* __restrict__ contrib,
-                                                           const float4* __restrict__ rec, gsr_grads g) {
+                                                           const float4* __restrict__ rec,
+                                                           const ushort4* __restrict__ rect,
+                                                           const uint64_t* __restrict__ cut, int gx, gsr_grads g) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= s.P) return;
     const int M = s.M;
@@ -300,21 +302,26 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         if (g.dsegments) { g.dsegments[2 * (size_t)idx] = 0.f; g.dsegments[2 * (size_t)idx + 1] = 0.f; }
         return;
     }
-    // gather-sum of the instance records, in slot order (deterministic)
+    // gather-sum of the instance records, in slot order (deterministic).  Slots
+    // follow the Gaussian's tile rectangle row by row (k_duplicate); a tile that
+    // stopped replaying before this Gaussian (sort key >= its cut) wrote no record.
+    const float4 r0 = rec[(size_t)idx * REC_F4], r1 = rec[(size_t)idx * REC_F4 + 1];
     float q[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) q[j] = 0.f;
     {
-        const uint32_t n = tiles_touched[idx];
+        const uint64_t key = ((uint64_t)__float_as_uint(r1.z) << 32) | (uint32_t)idx;
+        const ushort4 rc = rect[idx];
         const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)goff[idx] * 12);
-        for (uint32_t k = 0; k < n; ++k) {
-            const float4 a = src[3 * k], b = src[3 * k + 1], c = src[3 * k + 2];
-            q[0] += a.x; q[1] += a.y; q[2] += a.z; q[3] += a.w;
-            q[4] += b.x; q[5] += b.y; q[6] += b.z; q[7] += b.w;
-            q[8] += c.x; q[9] += c.y; q[10] += c.z; q[11] += c.w;
-        }
+        for (int y = rc.y; y < rc.w; ++y)
+            for (int x = rc.x; x < rc.z; ++x, src += 3) {
+                if (!(key < cut[y * gx + x])) continue;
+                const float4 a = src[0], b = src[1], c = src[2];
+                q[0] += a.x; q[1] += a.y; q[2] += a.z; q[3] += a.w;
+                q[4] += b.x; q[5] += b.y; q[6] += b.z; q[7] += b.w;
+                q[8] += c.x; q[9] += c.y; q[10] += c.z; q[11] += c.w;
+            }
     }
-    const float4 r0 = rec[(size_t)idx * REC_F4], r1 = rec[(size_t)idx * REC_F4 + 1];
     const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
     const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * s.W);
     const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * s.H);
@@ -564,10 +571,11 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const float4* rec, const gsr_grads& g, hipStream_t st) {
+                              const float* contrib, const float4* rec, const ushort4* rect, const uint64_t* cut,
+                              int gx, const gsr_grads& g, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_gaussian_backward, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, radii, tiles_touched,
-                       goff, clamped, contrib, rec, g);
+                       goff, clamped, contrib, rec, rect, cut, gx, g);
 }
 
 }  // namespace gsr

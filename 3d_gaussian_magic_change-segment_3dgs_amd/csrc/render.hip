@@ -343,7 +343,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                                                    const float* __restrict__ dL_dsegs,
                                                    const float* __restrict__ dL_ddepths,
                                                    const float* __restrict__ dL_dalphas,
-                                                   float* __restrict__ contrib) {
+                                                   float* __restrict__ contrib, uint64_t* __restrict__ cut) {
 #pragma clang fp contract(off)
     const int tile = (int)order[blockIdx.x];
     const int lane = threadIdx.x;
@@ -403,13 +403,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     STAT_DECL
     STAT(7, n);
     STAT(6, n > (int)maxlast ? n - (int)maxlast : 0);
-    // Instances behind every pixel's last contributor carry no gradient.
-    for (int p = (int)maxlast + lane; p < n; p += 64) {
-        float4* dst = reinterpret_cast<float4*>(contrib + (size_t)slot_vals[range.x + p] * 12);
-        const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-        dst[0] = z;
-        dst[1] = z;
-        dst[2] = z;
+    // Instances behind every pixel's last contributor carry no gradient and get
+    // no record: the tile publishes the (depth bits, id) sort key of its last
+    // replayed instance (+1; 0 = none) and k_gaussian_backward skips the slots of
+    // the tiles whose bound its own key does not stay below.
+    if (lane == 0) {
+        uint64_t c = 0;
+        if (maxlast > 0) {
+            const uint32_t gl = point_list[range.x + maxlast - 1];
+            const uint32_t dbits = __float_as_uint(rec[(size_t)gl * REC_F4 + 1].z);
+            c = (((uint64_t)dbits << 32) | gl) + 1;
+        }
+        cut[tile] = c;
     }
 
     // Same two-stage batch pipeline as the forward, walking the list back to front:
@@ -548,11 +553,11 @@ void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order,
                             const uint32_t* point_list, const uint32_t* slot_vals, const float4* rec,
                             const float* bg, const float* alpha, const uint32_t* n_contrib, const float* dL_dcolor,
                             const float* dL_dsegment, const float* dL_ddepth, const float* dL_dalpha, float* contrib,
-                            hipStream_t st) {
+                            uint64_t* cut, hipStream_t st) {
     const int T = gx * gy;
     if (T == 0) return;
     hipLaunchKernelGGL(k_render_bwd, dim3(T), dim3(64), 0, st, W, H, gx, order, ranges, point_list, slot_vals, rec,
-                       bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib);
+                       bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib, cut);
 }
 
 }  // namespace gsr

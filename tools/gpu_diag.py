@@ -76,6 +76,9 @@ def main():
     cases.append(("colors_precomp", sc, cam, dict(colors_precomp=cols)))
     # cov3D precomp from the scene's scale/rot (torch restatement)
     cases.append(("no_segments", sc, cam, dict(use_segments=False)))
+    if os.environ.get("DIAG_MT_PARITY"):
+        sc_mt, cam_mt = config_scene_and_camera("mt")
+        cases.append(("mt", sc_mt, cam_mt, {}))
     only = os.environ.get("DIAG_CASES")
     for name, s, c, kw in cases:
         if only and name not in only.split(","):
