@@ -121,7 +121,7 @@ size_t gsr_geom_bytes(int P) { return gsr::geom_layout(P > 0 ? (size_t)P : 0).by
 size_t gsr_binning_bytes(int num_rendered) { return gsr::bin_layout(num_rendered > 0 ? (size_t)num_rendered : 0).bytes; }
 size_t gsr_img_bytes(int W, int H) { return gsr::img_layout(W, H).bytes; }
 size_t gsr_backward_scratch_bytes(int num_rendered) {
-    return (num_rendered > 0 ? (size_t)num_rendered : 0) * 12 * sizeof(float) + gsr::ALIGN;
+    return gsr::scratch_layout(num_rendered > 0 ? (size_t)num_rendered : 0).bytes;
 }
 
 int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* stream,
@@ -255,25 +255,30 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
     const GeomLayout GL = geom_layout(P);
     char* g = aligned_base(geom);
     float* contrib = nullptr;
+    uint32_t* written = nullptr;
     if (I > 0) {
         if (!binning || !scratch) return fail("[gsr] binning/scratch buffer is NULL");
         const BinLayout BL = bin_layout(I);
         char* b = aligned_base(binning);
-        contrib = reinterpret_cast<float*>(aligned_base(scratch));
+        const ScratchLayout SL = scratch_layout(I);
+        char* sc0 = aligned_base(scratch);
+        contrib = reinterpret_cast<float*>(sc0 + SL.contrib);
+        written = reinterpret_cast<uint32_t*>(sc0 + SL.written);
         {
             StageScope sc(GSR_STAGE_RENDER_BWD, st);
+            if (hipMemsetAsync(written, 0, cdiv(I, 32) * 4, st) != hipSuccess)
+                return fail("[gsr] hipMemsetAsync failed");
             launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order), at<uint2>(im, IL.ranges),
                                    at<uint32_t>(b, BL.point_list), at<uint32_t>(b, BL.slot_vals),
                                    at<float4>(g, GL.rec), s->bg, alpha, at<uint32_t>(im, IL.n_contrib), dL_dcolor,
-                                   dL_dsegment, dL_ddepth, dL_dalpha, contrib, at<uint64_t>(im, IL.cut), st);
+                                   dL_dsegment, dL_ddepth, dL_dalpha, contrib, written, st);
         }
         GSR_STAGE("render backward");
     }
     {
         StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);
         launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
-                                 at<uint8_t>(g, GL.clamped), contrib, at<float4>(g, GL.rec),
-                                 at<ushort4>(g, GL.rect), at<uint64_t>(im, IL.cut), IL.gx, *grads, st);
+                                 at<uint8_t>(g, GL.clamped), contrib, written, at<float4>(g, GL.rec), *grads, st);
     }
     GSR_STAGE("gaussian backward");
     return 0;

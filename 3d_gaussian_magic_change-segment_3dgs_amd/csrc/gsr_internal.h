@@ -78,9 +78,23 @@ inline BinLayout bin_layout(size_t I) {
     return L;
 }
 
+// ---- backward scratch: per-instance gradient records + written-slot mask ----
+struct ScratchLayout {
+    size_t contrib, written, bytes;
+};
+inline ScratchLayout scratch_layout(size_t I) {
+    ScratchLayout L{};
+    size_t o = 0;
+    auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes); return r; };
+    L.contrib = take(I * 12 * sizeof(float));
+    L.written = take(cdiv(I, 32) * 4);
+    L.bytes = o + ALIGN;
+    return L;
+}
+
 // ---- image buffer (reference ImageState, rasterizer_impl.cu:173-179) ----
 struct ImgLayout {
-    size_t ranges, n_contrib, order, cut, bytes;
+    size_t ranges, n_contrib, order, bytes;
     int gx, gy;
 };
 inline ImgLayout img_layout(int W, int H) {
@@ -93,7 +107,6 @@ inline ImgLayout img_layout(int W, int H) {
     L.ranges = take(T * 8);
     L.n_contrib = take(T * TILE_PIX * 4);  // tile-major: [tile][local pixel]
     L.order = take(T * 4);                 // heavy-first tile schedule
-    L.cut = take(T * 8);                   // backward: key bound of the tile's replayed prefix
     L.bytes = o + ALIGN;
     return L;
 }
@@ -111,8 +124,8 @@ void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const float4* rec, const ushort4* rect, const uint64_t* cut,
-                              int gx, const gsr_grads& g, hipStream_t st);
+                              const float* contrib, const uint32_t* written, const float4* rec,
+                              const gsr_grads& g, hipStream_t st);
 // binning.hip
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL = identity*/, uint32_t* keys_tmp,
                        uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,
@@ -134,7 +147,7 @@ void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order,
                             const uint32_t* point_list,
                             const uint32_t* slot_vals, const float4* rec, const float* bg, const float* alpha,
                             const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_dsegment,
-                            const float* dL_ddepth, const float* dL_dalpha, float* contrib, uint64_t* cut,
+                            const float* dL_ddepth, const float* dL_dalpha, float* contrib, uint32_t* written,
                             hipStream_t st);
 
 uint32_t higher_msb(uint32_t n);

@@ -282,9 +282,8 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
                                                            const uint32_t* __restrict__ goff,
                                                            const uint8_t* __restrict__ clamped,
                                                            const float* __restrict__ contrib,
-                                                           const float4* __restrict__ rec,
-                                                           const ushort4* __restrict__ rect,
-                                                           const uint64_t* __restrict__ cut, int gx, gsr_grads g) {
+                                                           const uint32_t* __restrict__ written,
+                                                           const float4* __restrict__ rec, gsr_grads g) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= s.P) return;
     const int M = s.M;
@@ -302,25 +301,28 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         if (g.dsegments) { g.dsegments[2 * (size_t)idx] = 0.f; g.dsegments[2 * (size_t)idx + 1] = 0.f; }
         return;
     }
-    // gather-sum of the instance records, in slot order (deterministic).  Slots
-    // follow the Gaussian's tile rectangle row by row (k_duplicate); a tile that
-    // stopped replaying before this Gaussian (sort key >= its cut) wrote no record.
+    // gather-sum of the written instance records of the Gaussian's slot range
+    // [goff, goff + tiles_touched), in slot order (deterministic).
     const float4 r0 = rec[(size_t)idx * REC_F4], r1 = rec[(size_t)idx * REC_F4 + 1];
     float q[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) q[j] = 0.f;
     {
-        const uint64_t key = ((uint64_t)__float_as_uint(r1.z) << 32) | (uint32_t)idx;
-        const ushort4 rc = rect[idx];
-        const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)goff[idx] * 12);
-        for (int y = rc.y; y < rc.w; ++y)
-            for (int x = rc.x; x < rc.z; ++x, src += 3) {
-                if (!(key < cut[y * gx + x])) continue;
+        const uint32_t lo = goff[idx], hi = lo + tiles_touched[idx];
+        for (uint32_t w = lo >> 5; w <= (hi - 1) >> 5; ++w) {
+            uint32_t bits = written[w];
+            if (w == lo >> 5) bits &= ~0u << (lo & 31);
+            if (w == (hi - 1) >> 5 && ((hi & 31) != 0)) bits &= ~(~0u << (hi & 31));
+            while (bits) {
+                const uint32_t u = (w << 5) + (uint32_t)__builtin_ctz(bits);
+                bits &= bits - 1;
+                const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)u * 12);
                 const float4 a = src[0], b = src[1], c = src[2];
                 q[0] += a.x; q[1] += a.y; q[2] += a.z; q[3] += a.w;
                 q[4] += b.x; q[5] += b.y; q[6] += b.z; q[7] += b.w;
                 q[8] += c.x; q[9] += c.y; q[10] += c.z; q[11] += c.w;
             }
+        }
     }
     const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
     const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * s.W);
@@ -571,11 +573,11 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const float4* rec, const ushort4* rect, const uint64_t* cut,
-                              int gx, const gsr_grads& g, hipStream_t st) {
+                              const float* contrib, const uint32_t* written, const float4* rec,
+                              const gsr_grads& g, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_gaussian_backward, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, radii, tiles_touched,
-                       goff, clamped, contrib, rec, rect, cut, gx, g);
+                       goff, clamped, contrib, written, rec, g);
 }
 
 }  // namespace gsr

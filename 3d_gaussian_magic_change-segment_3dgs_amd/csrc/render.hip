@@ -18,9 +18,11 @@
 // pair, each lane sums its 4 pixels in registers, the wave reduces the 12
 // gradient channels with a transposed butterfly on v_permlane32_swap /
 // v_permlane16_swap / DPP (34 VALU ops, no LDS round trips), and 12 lanes
-// store ONE 48-B record per (tile, Gaussian) instance at the instance's slot.
-// The per-Gaussian backward kernel sums a Gaussian's slots in fixed order:
-// deterministic, atomic-free gradients.  Record (q = G * dL_dalpha per pixel,
+// store ONE 48-B record per replayed (tile, Gaussian) instance at the
+// instance's slot and set the slot's bit in a written-mask.  Instances that no
+// pixel replays (behind every last contributor, or out of reach) write nothing.
+// The per-Gaussian backward kernel sums a Gaussian's written slots in slot
+// order: deterministic, atomic-free gradients.  Record (q = G * dL_dalpha per pixel,
 // d = (dx, dy) = mean2D - pixel):
 //   [sum dch*dL_dcolor.rgb, sum dch*dL_dseg0/1, sum dch*dL_ddepth,
 //    sum q, sum q dx, sum q dy, sum q dx^2, sum q dx dy, sum q dy^2]
@@ -343,7 +345,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                                                    const float* __restrict__ dL_dsegs,
                                                    const float* __restrict__ dL_ddepths,
                                                    const float* __restrict__ dL_dalphas,
-                                                   float* __restrict__ contrib, uint64_t* __restrict__ cut) {
+                                                   float* __restrict__ contrib, uint32_t* __restrict__ written) {
 #pragma clang fp contract(off)
     const int tile = (int)order[blockIdx.x];
     const int lane = threadIdx.x;
@@ -403,20 +405,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     STAT_DECL
     STAT(7, n);
     STAT(6, n > (int)maxlast ? n - (int)maxlast : 0);
-    // Instances behind every pixel's last contributor carry no gradient and get
-    // no record: the tile publishes the (depth bits, id) sort key of its last
-    // replayed instance (+1; 0 = none) and k_gaussian_backward skips the slots of
-    // the tiles whose bound its own key does not stay below.
-    if (lane == 0) {
-        uint64_t c = 0;
-        if (maxlast > 0) {
-            const uint32_t gl = point_list[range.x + maxlast - 1];
-            const uint32_t dbits = __float_as_uint(rec[(size_t)gl * REC_F4 + 1].z);
-            c = (((uint64_t)dbits << 32) | gl) + 1;
-        }
-        cut[tile] = c;
-    }
-
     // Same two-stage batch pipeline as the forward, walking the list back to front:
     // lane l of the batch with upper end `top` owns position top-1-l.
     const int top0 = (int)maxlast;
@@ -442,13 +430,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
         u_cur = u_nxt;
         const float pmin = power_floor(rb.y);
         const bool hit = lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1);
-        if (lane < cnt && !hit) {  // no pixel of the tile can be reached: zero record, in parallel
-            float4* d4 = reinterpret_cast<float4*>(contrib + (size_t)uslot * 12);
-            const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-            d4[0] = z;
-            d4[1] = z;
-            d4[2] = z;
-        }
         uint64_t todo = __ballot(hit);
         STAT(2, cnt - __popcll(todo));
         while (todo) {
@@ -473,7 +454,6 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
             STAT(0, 1);
             if (!__any(near[0] | near[1] | near[2] | near[3])) {
                 STAT(1, 1);
-                if (lane < 12) dst[lane] = 0.f;
                 continue;
             }
             STAT(3, 1);
@@ -532,6 +512,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
             bool valid;
             const float r = wave_reduce12(acc, lane, vidx, valid);
             if (valid) dst[vidx] = r;
+            // Bit u marks slot u as written (order-independent OR: deterministic).
+            if (lane == 0) atomicOr(&written[u >> 5], 1u << (u & 31));
         }
     }
     STAT_FLUSH(16)
@@ -553,11 +535,11 @@ void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order,
                             const uint32_t* point_list, const uint32_t* slot_vals, const float4* rec,
                             const float* bg, const float* alpha, const uint32_t* n_contrib, const float* dL_dcolor,
                             const float* dL_dsegment, const float* dL_ddepth, const float* dL_dalpha, float* contrib,
-                            uint64_t* cut, hipStream_t st) {
+                            uint32_t* written, hipStream_t st) {
     const int T = gx * gy;
     if (T == 0) return;
     hipLaunchKernelGGL(k_render_bwd, dim3(T), dim3(64), 0, st, W, H, gx, order, ranges, point_list, slot_vals, rec,
-                       bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib, cut);
+                       bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib, written);
 }
 
 }  // namespace gsr
