@@ -146,37 +146,51 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_upsweep(const uint32_t* 
         if (idx < n) atomicAdd(&cnt[(keys[idx] >> shift) & mask], 1u);
     }
     __syncthreads();
-    hist[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = cnt[threadIdx.x];
+    if (threadIdx.x <= mask) hist[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = cnt[threadIdx.x];
 }
 
-// Stable scatter.  Elements are ranked round by round (256 per round, in index
-// order); inside a round, a wave64 multi-split by ballots gives each element its
-// rank among equal digits of its wave, and per-wave digit counts in LDS order the
-// four waves.  vals_in == NULL means value = element index.  An optional second
-// payload word (vals2) travels with the pair (NULL = none).
+// Stable scatter, staged through LDS.  Wave w of the block ranks the elements
+// [1024 w, 1024 w + 1024) of the block's tile in 16 rounds of 64: a wave64
+// multi-split by ballots gives each element its rank among equal digits of the
+// round, and a per-wave digit counter in LDS (read by all lanes, then bumped by
+// the digit's first lane -- ordered within the wave, no barrier) carries the
+// rank across rounds.  One block scan then turns the 4 x 2^bits counters into
+// block-local digit bases, the tile is permuted into digit order in LDS, and
+// written out with consecutive threads on consecutive positions of each digit's
+// run (coalesced, unlike a direct per-element scatter).  Stable: element order
+// inside a digit is (wave, round, lane) = input order.  vals_in == NULL means
+// value = element index; vals2 is an optional second payload word.
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, size_t n, int shift, int bits, const uint32_t* __restrict__ hist,
     const uint32_t* __restrict__ vals2_in, uint32_t* __restrict__ vals2_out) {
-    __shared__ uint32_t base_off[RADIX];
+    __shared__ uint32_t s_key[SORT_TILE], s_val[SORT_TILE], s_val2[SORT_TILE];
     __shared__ uint32_t wcnt[4][RADIX];
+    __shared__ uint32_t dbase[RADIX], gbase[RADIX];
+    __shared__ uint32_t wsum[4];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const uint32_t mask = (1u << bits) - 1u;
-    base_off[tid] = hist[(size_t)tid * gridDim.x + blockIdx.x];
-    const size_t base = (size_t)blockIdx.x * SORT_TILE;
-    const uint64_t lt = lanemask_lt();
-    for (int r = 0; r < SORT_ITEMS; ++r) {
+    const uint32_t ndig = 1u << bits, mask = ndig - 1u;
+    const int nb = (int)gridDim.x;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) wcnt[w][tid] = 0;
-        const size_t idx = base + (size_t)r * SORT_THREADS + tid;
+    for (int i = 0; i < RADIX / 64; ++i) wcnt[wid][lane + 64 * i] = 0;
+    if ((uint32_t)tid < ndig) gbase[tid] = hist[(size_t)tid * nb + blockIdx.x];
+    const size_t bbase = (size_t)blockIdx.x * SORT_TILE;
+    const size_t wbase = bbase + (size_t)wid * (SORT_TILE / 4);
+    const uint64_t lt = lanemask_lt();
+    uint32_t key[SORT_ITEMS], val[SORT_ITEMS], val2[SORT_ITEMS], rk[SORT_ITEMS];
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; ++r) {
+        const size_t idx = wbase + (size_t)r * 64 + lane;
         const bool valid = idx < n;
-        uint32_t key = 0, val = 0, val2 = 0, digit = 0;
-        if (valid) {
-            key = keys_in[idx];
-            val = vals_in ? vals_in[idx] : (uint32_t)idx;
-            if (vals2_in) val2 = vals2_in[idx];
-            digit = (key >> shift) & mask;
-        }
+        key[r] = valid ? keys_in[idx] : 0u;
+        val[r] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+        val2[r] = (valid && vals2_in) ? vals2_in[idx] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; ++r) {
+        const size_t idx = wbase + (size_t)r * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t digit = (key[r] >> shift) & mask;
         uint64_t peers = __ballot(valid);
         for (int b = 0; b < bits; ++b) {
             const bool set = (digit >> b) & 1u;
@@ -184,20 +198,49 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
             peers &= set ? m : ~m;
         }
         const uint32_t rank = __popcll(peers & lt);
-        const uint32_t wtotal = __popcll(peers);
-        __syncthreads();  // wcnt zeroed
-        if (valid && rank == 0) wcnt[wid][digit] = wtotal;
-        __syncthreads();
-        if (valid) {
-            uint32_t pos = base_off[digit] + rank;
-            for (int w = 0; w < wid; ++w) pos += wcnt[w][digit];
-            keys_out[pos] = key;
-            vals_out[pos] = val;
-            if (vals2_out) vals2_out[pos] = val2;
+        const uint32_t old = valid ? wcnt[wid][digit] : 0u;
+        rk[r] = old + rank;
+        if (valid && rank == 0) wcnt[wid][digit] = old + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    // digit-major block offsets: dbase[d] = elements of digits < d; wave offsets inside d
+    uint32_t c[4], tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+        c[w] = (uint32_t)tid < ndig ? wcnt[w][tid] : 0u;
+        tot += c[w];
+    }
+    uint32_t total;
+    const uint32_t db = block_exclusive_scan(tot, wsum, &total);
+    if ((uint32_t)tid < ndig) {
+        dbase[tid] = db;
+        uint32_t o = db;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+            wcnt[w][tid] = o;
+            o += c[w];
         }
-        __syncthreads();
-        base_off[tid] += wcnt[0][tid] + wcnt[1][tid] + wcnt[2][tid] + wcnt[3][tid];
-        __syncthreads();
+    }
+    __syncthreads();
+#pragma unroll
+    for (int r = 0; r < SORT_ITEMS; ++r) {
+        const size_t idx = wbase + (size_t)r * 64 + lane;
+        if (idx < n) {
+            const uint32_t pos = wcnt[wid][(key[r] >> shift) & mask] + rk[r];
+            s_key[pos] = key[r];
+            s_val[pos] = val[r];
+            s_val2[pos] = val2[r];
+        }
+    }
+    __syncthreads();
+    const int nvalid = (int)min((size_t)SORT_TILE, n - bbase);
+    for (int p = tid; p < nvalid; p += SORT_THREADS) {
+        const uint32_t k = s_key[p];
+        const uint32_t d = (k >> shift) & mask;
+        const size_t g = (size_t)gbase[d] + (uint32_t)p - dbase[d];
+        keys_out[g] = k;
+        vals_out[g] = s_val[p];
+        if (vals2_out) vals2_out[g] = s_val2[p];
     }
 }
 
@@ -309,13 +352,14 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     if (n == 0) return;
     if (key_bits < 1) key_bits = 1;
     const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
+    const int per_pass = (key_bits + passes - 1) / passes;  // balanced: 13 bits -> 7 + 6
     const size_t nb = sort_blocks(n);
     const uint32_t* kin = keys_in;
     const uint32_t* vin = vals_in;
     const uint32_t* v2in = vals2_in;
     for (int p = 0; p < passes; ++p) {
-        const int shift = p * RADIX_BITS;
-        const int bits = key_bits - shift < RADIX_BITS ? key_bits - shift : RADIX_BITS;
+        const int shift = p * per_pass;
+        const int bits = key_bits - shift < per_pass ? key_bits - shift : per_pass;
         // last pass writes the output pair; earlier passes alternate so that holds
         const bool to_out = ((passes - 1 - p) % 2) == 0;
         uint32_t* kout = to_out ? keys_out : keys_tmp;
@@ -323,7 +367,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
         uint32_t* v2out = vals2_in ? (to_out ? vals2_out : vals2_tmp) : nullptr;
         hipLaunchKernelGGL(k_radix_upsweep, dim3(nb), dim3(SORT_THREADS), 0, st, kin, n, shift,
                            (1u << bits) - 1u, hist);
-        scan_exclusive_inplace(hist, (size_t)RADIX * nb, parts, st);
+        scan_exclusive_inplace(hist, ((size_t)1 << bits) * nb, parts, st);
         hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, st, kin, vin, kout, vout, n, shift,
                            bits, hist, v2in, v2out);
         kin = kout;
