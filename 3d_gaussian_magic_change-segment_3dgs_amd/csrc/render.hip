@@ -35,7 +35,7 @@
 // sensitive to exp(), and the reference's backward recovers T from
 // T_final = 1 - sum(alpha*T) (backward.cu:468), amplifying any last-ulp alpha
 // difference by 1/T_final.  gsr therefore evaluates exp() with gsr_expf below:
-// IEEE operations only (mul, rint, fma, ldexp), so the CPU oracle computes the
+// IEEE operations only (fma, add, mul, integer shift), so the CPU oracle computes the
 // very same bits (oracle/gsr_oracle.cpp: gsr_expf).  Max error 0.88 ulp,
 // correctly rounded on 99.55% of inputs (tests/test_oracle_golden.py pins it
 // against double-precision exp; the reference's CUDA expf is specified at 2 ulp).
@@ -43,9 +43,16 @@
 // power, alpha, T and the weight sum run without FMA contraction (see the
 // kernels); only non-amplified sums use explicit FMAs.
 __device__ __forceinline__ float gsr_expf(float x) {
-    const float xc = fminf(fmaxf(x, -104.0f), 88.72283935546875f);
-    const float k = __builtin_rintf(xc * 1.44269502f);
-    float r = __builtin_fmaf(-k, 0.693145751953125f, xc);  // Cody-Waite ln2 = hi + lo
+    // exp(clamp(x, -87, 88)).  k = round(x log2 e) via the 1.5*2^23 shifter (one FMA,
+    // the integer lands in the low mantissa bits), Cody-Waite ln2 = hi + lo, degree-7
+    // Taylor polynomial in Horner form, then times 2^k assembled from the shifter's
+    // bits (k in [-126, 127], so the product is an exact scaling).  Outside the clamp
+    // the value is meaningless for blending anyway: alpha < 1/255 below -87 and the
+    // blend rejects power > 0.
+    const float xc = __builtin_amdgcn_fmed3f(x, -87.0f, 88.0f);
+    const float kf = __builtin_fmaf(xc, 1.44269502f, 12582912.0f);
+    const float k = kf - 12582912.0f;
+    float r = __builtin_fmaf(-k, 0.693145751953125f, xc);
     r = __builtin_fmaf(-k, 1.42860677e-06f, r);
     float p = 1.98412701e-04f;                  // 1/7!, Horner with FMAs
     p = __builtin_fmaf(p, r, 1.38888892e-03f);  // 1/6!
@@ -55,8 +62,8 @@ __device__ __forceinline__ float gsr_expf(float x) {
     p = __builtin_fmaf(p, r, 0.5f);
     p = __builtin_fmaf(p, r, 1.0f);
     p = __builtin_fmaf(p, r, 1.0f);
-    const float v = __builtin_ldexpf(p, (int)k);
-    return x < -104.0f ? 0.0f : (x > 88.72283935546875f ? __builtin_inff() : v);
+    const float scale = __uint_as_float((__float_as_uint(kf) << 23) + 0x3f800000u);
+    return p * scale;
 }
 #ifdef GSR_FAST_EXP
 #define GSR_EXP(x) __expf(x)

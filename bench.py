@@ -38,27 +38,27 @@ PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1_pmc_summary.json")
 
 
 def algorithmic_bytes(stage, P, I, HW, deg, launches_per_view=1):
-    """Bytes a stage must move per launch (DESIGN.md s4 lists the derivation)."""
-    ncoef = (deg + 1) ** 2
-    sh = 12 * ncoef
-    if stage == "preprocess":      # means,scales,rot,opac,seg,SH in; record,radii,tiles,key,clamp,rect out
-        return P * (12 + 12 + 16 + 4 + 8 + sh + 64 + 4 + 4 + 4 + 1 + 8)
-    if stage == "render_fwd":      # per instance: id + 48-B record; per pixel: 8 outputs + n_contrib
-        return I * (4 + 48) + HW * (12 + 4 + 4 + 8 + 4)
-    if stage == "render_bwd":      # per instance: id + slot + record in, 48-B gradient record out; per pixel ins
-        return I * (4 + 4 + 48 + 48) + HW * (4 + 4 + 12 + 8 + 4 + 4)
-    if stage == "gaussian_bwd":    # gradient records in + per-Gaussian params/SH in + all grads out
-        return I * 48 + P * (13 + 12 + 12 + 16 + sh + 12 + 4 + 12 + sh + 12 + 16 + 8)
-    if stage == "duplicate":       # order/offset/tiles/rect in; key + owner out per instance
-        return P * (4 + 4 + 4 + 8 + 4) + I * 8
-    if stage == "tile_sort":       # per pass: key+val in and out (first pass: no val in) + key re-read
-        return I * (4 + 8 + 8 + 8 + 4)
-    if stage == "ranges":
-        return I * (4 + 4 + 4 + 4 + 4)
-    if stage == "depth_sort":
-        return P * (4 + 8 + 3 * (8 + 8) + 8 + 4 * 4)
-    if stage == "scan":
-        return P * (4 + 4 + 4 + 4)
+    """Bytes a stage must move per launch: SURVEY.md s8(d)'s per-unit figures
+    (a7..a16) attributed to the gsr stage that does that work."""
+    M = (deg + 1) ** 2
+    if stage == "preprocess":      # a7: (119 + 12 M) B per Gaussian
+        return (119 + 12 * M) * P
+    if stage == "scan":            # a8
+        return 8 * P
+    if stage == "depth_sort":      # gsr-only stage: one read + write of (key, id) per Gaussian
+        return 16 * P
+    if stage == "duplicate":       # a9: 20 B per Gaussian + 12 B per instance
+        return 20 * P + 12 * I
+    if stage == "tile_sort":       # a10: one read + write of key + value per instance
+        return 24 * I
+    if stage == "ranges":          # a11
+        return 8 * I
+    if stage == "render_fwd":      # a12: 52 B per instance + 32 B per pixel
+        return 52 * I + 32 * HW
+    if stage == "render_bwd":      # a14 (per-instance + per-pixel part)
+        return 52 * I + 36 * HW
+    if stage == "gaussian_bwd":    # a14 grad outs + a15 + a16: 56 + 92 + (151 + 24 M) B per Gaussian
+        return (56 + 92 + 151 + 24 * M) * P
     return 0
 
 

@@ -262,13 +262,17 @@ static std::string g_err;
 
 // exp() of the blend (forward.cu:351, backward.cu:547).  The reference calls CUDA's
 // expf (2 ulp); gsr's kernels and this oracle share gsr_expf: IEEE operations only
-// (mul, rint, fma, ldexp), max 0.88 ulp, so both compute identical bits and the
+// (fma, add, mul, integer shift), max 0.88 ulp, so both compute identical bits and the
 // knife-edge blend decisions (alpha >= 1/255, T(1-alpha) >= 1e-4) agree exactly.
 // g_exp_libm = 1 switches to the C library's expf (noise-floor studies).
 static int g_exp_libm = 0;
 static inline float gsr_expf(float x) {
-    const float xc = std::fmin(std::fmax(x, -104.0f), 88.72283935546875f);
-    const float k = std::rint(xc * 1.44269502f);
+    // exp(clamp(x, -87, 88)): k = round(x log2 e) by the 1.5*2^23 shifter, Cody-Waite
+    // reduction, degree-7 Taylor polynomial (Horner, FMA), times 2^k built from the
+    // shifter's low bits.  Must stay bit-identical to render.hip: gsr_expf.
+    const float xc = std::fmin(std::fmax(x, -87.0f), 88.0f);
+    const float kf = std::fma(xc, 1.44269502f, 12582912.0f);
+    const float k = kf - 12582912.0f;
     float r = std::fma(-k, 0.693145751953125f, xc);
     r = std::fma(-k, 1.42860677e-06f, r);
     float p = 1.98412701e-04f;
@@ -279,8 +283,12 @@ static inline float gsr_expf(float x) {
     p = std::fma(p, r, 0.5f);
     p = std::fma(p, r, 1.0f);
     p = std::fma(p, r, 1.0f);
-    const float v = std::ldexp(p, (int)k);
-    return x < -104.0f ? 0.0f : (x > 88.72283935546875f ? INFINITY : v);
+    uint32_t kb;
+    std::memcpy(&kb, &kf, 4);
+    const uint32_t sb = (kb << 23) + 0x3f800000u;  // 2^k, k in [-126, 127]
+    float scale;
+    std::memcpy(&scale, &sb, 4);
+    return p * scale;
 }
 static inline float oracle_exp(float x) { return g_exp_libm ? std::exp(x) : gsr_expf(x); }
 // 1: emulate the reference's fp32 accumulation (one fixed order of its atomics)
