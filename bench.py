@@ -13,7 +13,9 @@ Prints ONE JSON line on rank 0.  Extra objects:
   roofline     -- the dominant kernel (per-stage HIP events recorded by libgsr on
                   the stream it launches on): algorithmic bytes per launch / mean
                   launch time vs the 8 TB/s HBM peak; `traffic` = PMC-measured HBM
-                  bytes per launch from profiles/ when a counter profile exists.
+                  bytes per launch from profiles/ when a counter profile exists;
+                  `valu_issue_frac` = PMC SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x
+                  2.4 GHz x launch time): the bound the render kernels actually hit.
   cpu_baseline -- the CPU oracle (C++ restatement of the reference kernels,
                   OpenMP) timed on this box's host cores on a bounded sample of the
                   same workload (whole views, rank 0, N = 1 only).
@@ -34,6 +36,7 @@ for p in (ROOT, PKG):
 import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
+SIMD_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1_pmc_summary.json")
 
 
@@ -190,17 +193,21 @@ def main():
     roof = None
     if dom:
         achieved = stages[dom]["gbs"]
-        traffic = None
+        traffic = valu_frac = None
         if os.path.exists(PMC_SUMMARY):
             try:
-                pm = json.load(open(PMC_SUMMARY))
-                traffic = pm.get("kernels", {}).get(dom, {}).get("hbm_bytes_per_launch")
+                pk = json.load(open(PMC_SUMMARY)).get("kernels", {}).get(dom, {})
+                traffic = pk.get("hbm_bytes_per_launch")
+                if pk.get("SQ_INSTS_VALU"):
+                    # wave64 VALU issue = 4 cycles on one of 1024 SIMDs, at the 2.4 GHz peak clock
+                    valu_frac = round(pk["SQ_INSTS_VALU"] * 4 / 1024 / (SIMD_CLOCK_HZ * stages[dom]["avg_ms"] * 1e-3), 4)
             except Exception:
-                traffic = None
+                traffic = valu_frac = None
         roof = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg),
                 "avg_launch_ms": stages[dom]["avg_ms"],
+                "valu_issue_frac": valu_frac,
                 "whole_view_frac": round(view_bytes(P, I, HW, deg) * value / world / 1e9 / HBM_PEAK_GBS, 4)}
     out = {
         "metric": "forward+backward views/sec @1080p, 1M Gaussians, 1/2/4/8 MI355X",
