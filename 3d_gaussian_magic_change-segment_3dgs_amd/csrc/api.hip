@@ -150,13 +150,13 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
         StageScope sc(GSR_STAGE_DEPTH_SORT, st);
         launch_radix_sort(at<uint32_t>(g, L.depth_keys), nullptr, at<uint32_t>(g, L.dkeys_alt),
                           at<uint32_t>(g, L.order_alt), at<uint32_t>(g, L.depth_keys), at<uint32_t>(g, L.order), P,
-                          32, at<uint32_t>(g, L.hist), at<uint32_t>(g, L.parts), st);
+                          32, g + L.ws, st);
     }
     GSR_STAGE("depth sort");
     {
         StageScope sc(GSR_STAGE_SCAN, st);
         launch_scan_inclusive_gather(at<uint32_t>(g, L.tiles_touched), at<uint32_t>(g, L.order),
-                                     at<uint32_t>(g, L.offsets), P, at<uint32_t>(g, L.parts), st);
+                                     at<uint32_t>(g, L.offsets), P, g + L.ws, st);
     }
     GSR_STAGE("scan");
     uint32_t total = 0;
@@ -211,7 +211,7 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
             // (depth, gaussian); the id travels along so point_list needs no gather.
             StageScope sc(GSR_STAGE_TILE_SORT, st);
             launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout, at<uint32_t>(b, BL.slot_vals),
-                              I, bits, at<uint32_t>(b, BL.hist), at<uint32_t>(b, BL.parts), st,
+                              I, bits, b + BL.ws, st,
                               at<uint32_t>(b, BL.slot_gid), at<uint32_t>(b, BL.gid_alt),
                               at<uint32_t>(b, BL.point_list));
         }

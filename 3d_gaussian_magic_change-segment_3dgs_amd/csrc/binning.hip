@@ -48,138 +48,215 @@ __device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* w
     return pre + x - v;
 }
 
+// ------------------------------------------------- decoupled look-back ----
+// Single-pass prefix sums (scan, radix scatter) publish one 64-bit status word per
+// (tile, lane of the sum): flag in the high half (1 = tile aggregate, 2 = inclusive
+// prefix), value in the low half.  Tiles take their index from an atomic counter in
+// launch order, so every tile a block waits on has already started: the spin always
+// terminates.  Status words are zeroed (memset) before each launch.  A status word
+// carries its own payload, so relaxed agent-scope atomics suffice: they are coherent
+// across the XCDs' L2s (sc1) without the L2 write-back / invalidate that
+// release / acquire ordering costs on MI355X.
+constexpr uint64_t LB_AGG = 1ull << 32, LB_PRE = 2ull << 32;
+__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint64_t lb_load(uint64_t* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Sum of the values of tiles 0..t-1 of one column (stride between tiles).
+__device__ __forceinline__ uint32_t lb_lookback(uint64_t* col, size_t stride, int t) {
+    uint32_t excl = 0;
+    int i = t - 1;
+    while (i >= 0) {
+        const uint64_t w = lb_load(col + (size_t)i * stride);
+        const uint32_t f = (uint32_t)(w >> 32);
+        if (f == 0) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        excl += (uint32_t)w;
+        if (f == 2) break;
+        --i;
+    }
+    return excl;
+}
+__device__ __forceinline__ int lb_tile_index(uint32_t* counter) {
+    __shared__ int s_tile;
+    if (threadIdx.x == 0) s_tile = (int)atomicAdd(counter, 1u);
+    __syncthreads();
+    return s_tile;
+}
+
 // ---------------------------------------------------------------- scan ----
-// value(i) = gather ? src[gather[i]] : src[i]
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_reduce(const uint32_t* __restrict__ src,
-                                                              const uint32_t* __restrict__ gather, size_t n,
-                                                              uint32_t* __restrict__ parts) {
-    __shared__ uint32_t wsum[4];
-    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
-    uint32_t acc = 0;
-#pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        size_t idx = base + (size_t)i * SCAN_THREADS + threadIdx.x;
-        if (idx < n) acc += gather ? src[gather[idx]] : src[idx];
-    }
-    uint32_t tot;
-    block_exclusive_scan(acc, wsum, &tot);
-    if (threadIdx.x == 0) parts[blockIdx.x] = tot;
-}
-
-// Single block: exclusive scan of parts[0..np) in place.
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_parts(uint32_t* __restrict__ parts, size_t np) {
-    __shared__ uint32_t wsum[4];
-    uint32_t carry = 0;
-    for (size_t base = 0; base < np; base += (size_t)SCAN_THREADS * SCAN_ITEMS) {
-        uint32_t v[SCAN_ITEMS];
-        uint32_t s = 0;
-        const size_t mine = base + (size_t)threadIdx.x * SCAN_ITEMS;
-#pragma unroll
-        for (int i = 0; i < SCAN_ITEMS; ++i) {
-            v[i] = (mine + i < np) ? parts[mine + i] : 0u;
-            s += v[i];
-        }
-        uint32_t tot;
-        uint32_t pre = block_exclusive_scan(s, wsum, &tot) + carry;
-#pragma unroll
-        for (int i = 0; i < SCAN_ITEMS; ++i) {
-            if (mine + i < np) parts[mine + i] = pre;
-            pre += v[i];
-        }
-        carry += tot;
-    }
-}
-
-// out[i] = (inclusive ? sum_{j<=i} : sum_{j<i}) value(j); tile staged through LDS so
-// both the loads and the stores are coalesced.
+// out[i] = sum_{j<=i (INCLUSIVE) / j<i} value(j), value(j) = gather ? src[gather[j]] : src[j], in one
+// pass: each tile of 4096 values is staged through LDS (coalesced loads/stores),
+// reduced, its prefix found by look-back, then scanned.
 template <bool INCLUSIVE>
-__global__ void __launch_bounds__(SCAN_THREADS) k_scan_down(const uint32_t* __restrict__ src,
-                                                            const uint32_t* __restrict__ gather, size_t n,
-                                                            const uint32_t* __restrict__ parts,
-                                                            uint32_t* __restrict__ out) {
+__global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restrict__ src,
+                                                       const uint32_t* __restrict__ gather, size_t n,
+                                                       uint32_t* __restrict__ out, uint64_t* status,
+                                                       uint32_t* counter) {
     __shared__ uint32_t tile[SCAN_TILE + SCAN_TILE / 32];
     __shared__ uint32_t wsum[4];
-    const size_t base = (size_t)blockIdx.x * SCAN_TILE;
+    __shared__ uint32_t s_excl;
+    const int t = lb_tile_index(counter);
+    const size_t base = (size_t)t * SCAN_TILE;
     auto pad = [](int i) { return i + (i >> 5); };
+    uint32_t v[SCAN_ITEMS], sum = 0;
+    if (gather) {
+        uint32_t gi[SCAN_ITEMS];
 #pragma unroll
-    for (int i = 0; i < SCAN_ITEMS; ++i) {
-        int li = i * SCAN_THREADS + threadIdx.x;
-        size_t idx = base + li;
-        tile[pad(li)] = idx < n ? (gather ? src[gather[idx]] : src[idx]) : 0u;
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            const size_t idx = base + i * SCAN_THREADS + threadIdx.x;
+            gi[i] = idx < n ? gather[idx] : 0u;
+        }
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            const size_t idx = base + i * SCAN_THREADS + threadIdx.x;
+            v[i] = idx < n ? src[gi[i]] : 0u;
+        }
+    } else {
+#pragma unroll
+        for (int i = 0; i < SCAN_ITEMS; ++i) {
+            const size_t idx = base + i * SCAN_THREADS + threadIdx.x;
+            v[i] = idx < n ? src[idx] : 0u;
+        }
     }
+#pragma unroll
+    for (int i = 0; i < SCAN_ITEMS; ++i) tile[pad(i * SCAN_THREADS + threadIdx.x)] = v[i];
     __syncthreads();
-    uint32_t v[SCAN_ITEMS], s = 0;
 #pragma unroll
     for (int i = 0; i < SCAN_ITEMS; ++i) {
         v[i] = tile[pad(threadIdx.x * SCAN_ITEMS + i)];
-        s += v[i];
+        sum += v[i];
     }
-    uint32_t tot;
-    uint32_t pre = block_exclusive_scan(s, wsum, &tot) + parts[blockIdx.x];
+    uint32_t total;
+    uint32_t pre = block_exclusive_scan(sum, wsum, &total);
+    if (threadIdx.x == 0) {
+        uint32_t excl = 0;
+        if (t == 0) {
+            lb_store(status, LB_PRE | total);
+        } else {
+            lb_store(status + t, LB_AGG | total);
+            excl = lb_lookback(status, 1, t);
+            lb_store(status + t, LB_PRE | (excl + total));
+        }
+        s_excl = excl;
+    }
+    __syncthreads();
+    pre += s_excl;
 #pragma unroll
     for (int i = 0; i < SCAN_ITEMS; ++i) {
-        uint32_t nx = pre + v[i];
+        const uint32_t nx = pre + v[i];
         tile[pad(threadIdx.x * SCAN_ITEMS + i)] = INCLUSIVE ? nx : pre;
         pre = nx;
     }
     __syncthreads();
 #pragma unroll
     for (int i = 0; i < SCAN_ITEMS; ++i) {
-        int li = i * SCAN_THREADS + threadIdx.x;
-        size_t idx = base + li;
+        const int li = i * SCAN_THREADS + threadIdx.x;
+        const size_t idx = base + li;
         if (idx < n) out[idx] = tile[pad(li)];
     }
 }
 
 // ---------------------------------------------------------- radix sort ----
-// Per-block digit histogram -> hist[digit * nblocks + block].
-__global__ void __launch_bounds__(SORT_THREADS) k_radix_upsweep(const uint32_t* __restrict__ keys, size_t n,
-                                                                int shift, uint32_t mask,
-                                                                uint32_t* __restrict__ hist) {
-    __shared__ uint32_t cnt[RADIX];
-    cnt[threadIdx.x] = 0;
-    __syncthreads();
-    const size_t base = (size_t)blockIdx.x * SORT_TILE;
+// Digit histograms of every pass at once (one read of the keys): LDS counters per
+// block, then one global atomic per (pass, digit, block).  hist[p * RADIX + d].
+__global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __restrict__ keys, size_t n,
+                                                             int passes, int per_pass, int key_bits,
+                                                             uint32_t* __restrict__ hist) {
+    __shared__ uint32_t cnt[4][RADIX];
 #pragma unroll
-    for (int i = 0; i < SORT_ITEMS; ++i) {
-        size_t idx = base + (size_t)i * SORT_THREADS + threadIdx.x;
-        if (idx < n) atomicAdd(&cnt[(keys[idx] >> shift) & mask], 1u);
+    for (int p = 0; p < 4; ++p) cnt[p][threadIdx.x] = 0;
+    __syncthreads();
+    for (size_t idx = (size_t)blockIdx.x * SORT_THREADS + threadIdx.x; idx < n;
+         idx += (size_t)gridDim.x * SORT_THREADS) {
+        const uint32_t k = keys[idx];
+        for (int p = 0; p < passes; ++p) {
+            const int shift = p * per_pass;
+            const int bits = min(per_pass, key_bits - shift);
+            atomicAdd(&cnt[p][(k >> shift) & ((1u << bits) - 1u)], 1u);
+        }
     }
     __syncthreads();
-    if (threadIdx.x <= mask) hist[(size_t)threadIdx.x * gridDim.x + blockIdx.x] = cnt[threadIdx.x];
+    for (int p = 0; p < passes; ++p)
+        if (cnt[p][threadIdx.x]) atomicAdd(&hist[p * RADIX + threadIdx.x], cnt[p][threadIdx.x]);
 }
 
-// Stable scatter, staged through LDS.  Wave w of the block ranks the elements
+// Per-tile digit histogram -> hist[digit * ntiles + tile] (table-driven passes).
+// Equal digits of a wave round are counted by their first lane (ballot multisplit),
+// so skewed digit distributions do not serialise on one LDS address.
+template <int ITEMS>
+__global__ void __launch_bounds__(SORT_THREADS) k_radix_upsweep(const uint32_t* __restrict__ keys, size_t n,
+                                                                int shift, int bits, uint32_t* __restrict__ hist) {
+    __shared__ uint32_t cnt[RADIX];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const uint32_t ndig = 1u << bits, mask = ndig - 1u;
+    cnt[tid] = 0;
+    __syncthreads();
+    const size_t wbase = (size_t)blockIdx.x * (SORT_THREADS * ITEMS) + (size_t)wid * (64 * ITEMS);
+    uint32_t key[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const size_t idx = wbase + (size_t)r * 64 + lane;
+        key[r] = idx < n ? keys[idx] : 0u;
+    }
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const bool valid = wbase + (size_t)r * 64 + lane < n;
+        const uint32_t digit = (key[r] >> shift) & mask;
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < bits; ++b) {
+            const bool set = (digit >> b) & 1u;
+            const uint64_t m = __ballot(set);
+            peers &= set ? m : ~m;
+        }
+        if (valid && __popcll(peers & lanemask_lt()) == 0) atomicAdd(&cnt[digit], (uint32_t)__popcll(peers));
+    }
+    __syncthreads();
+    if ((uint32_t)tid < ndig) hist[(size_t)tid * gridDim.x + blockIdx.x] = cnt[tid];
+}
+
+// Stable scatter, staged through LDS, one launch per pass.  Wave w of the tile ranks the elements
 // [1024 w, 1024 w + 1024) of the block's tile in 16 rounds of 64: a wave64
 // multi-split by ballots gives each element its rank among equal digits of the
 // round, and a per-wave digit counter in LDS (read by all lanes, then bumped by
 // the digit's first lane -- ordered within the wave, no barrier) carries the
 // rank across rounds.  One block scan then turns the 4 x 2^bits counters into
-// block-local digit bases, the tile is permuted into digit order in LDS, and
+// block-local digit bases, a decoupled look-back over earlier tiles (per digit)
+// gives the tile's global digit offsets, the tile is permuted into digit order in LDS, and
 // written out with consecutive threads on consecutive positions of each digit's
 // run (coalesced, unlike a direct per-element scatter).  Stable: element order
 // inside a digit is (wave, round, lane) = input order.  vals_in == NULL means
 // value = element index; vals2 is an optional second payload word.
+// LB = true: the tile's global digit offsets come from a decoupled look-back over
+// earlier tiles (one launch per pass; hist = the pass's global digit histogram).
+// LB = false: they come from a scanned per-tile histogram table (hist[d * ntiles + t],
+// k_radix_upsweep + k_scan<false>): more launches, but no look-back latency chain,
+// which costs a cross-XCD round trip per hop on MI355X.
+template <int ITEMS, bool LB>
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, size_t n, int shift, int bits, const uint32_t* __restrict__ hist,
-    const uint32_t* __restrict__ vals2_in, uint32_t* __restrict__ vals2_out) {
-    __shared__ uint32_t s_key[SORT_TILE], s_val[SORT_TILE], s_val2[SORT_TILE];
+    uint64_t* status, uint32_t* counter, const uint32_t* __restrict__ vals2_in, uint32_t* __restrict__ vals2_out) {
+    constexpr int TILE = SORT_THREADS * ITEMS;
+    __shared__ uint32_t s_key[TILE], s_val[TILE], s_val2[TILE];
     __shared__ uint32_t wcnt[4][RADIX];
     __shared__ uint32_t dbase[RADIX], gbase[RADIX];
     __shared__ uint32_t wsum[4];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t ndig = 1u << bits, mask = ndig - 1u;
-    const int nb = (int)gridDim.x;
+    const int t = LB ? lb_tile_index(counter) : (int)blockIdx.x;
 #pragma unroll
     for (int i = 0; i < RADIX / 64; ++i) wcnt[wid][lane + 64 * i] = 0;
-    if ((uint32_t)tid < ndig) gbase[tid] = hist[(size_t)tid * nb + blockIdx.x];
-    const size_t bbase = (size_t)blockIdx.x * SORT_TILE;
-    const size_t wbase = bbase + (size_t)wid * (SORT_TILE / 4);
+    const size_t bbase = (size_t)t * TILE;
+    const size_t wbase = bbase + (size_t)wid * (TILE / 4);
     const uint64_t lt = lanemask_lt();
-    uint32_t key[SORT_ITEMS], val[SORT_ITEMS], val2[SORT_ITEMS], rk[SORT_ITEMS];
+    uint32_t key[ITEMS], val[ITEMS], val2[ITEMS], rk[ITEMS];
 #pragma unroll
-    for (int r = 0; r < SORT_ITEMS; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const size_t idx = wbase + (size_t)r * 64 + lane;
         const bool valid = idx < n;
         key[r] = valid ? keys_in[idx] : 0u;
@@ -187,7 +264,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
         val2[r] = (valid && vals2_in) ? vals2_in[idx] : 0u;
     }
 #pragma unroll
-    for (int r = 0; r < SORT_ITEMS; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const size_t idx = wbase + (size_t)r * 64 + lane;
         const bool valid = idx < n;
         const uint32_t digit = (key[r] >> shift) & mask;
@@ -212,6 +289,8 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
     }
     uint32_t total;
     const uint32_t db = block_exclusive_scan(tot, wsum, &total);
+    // global start of each digit (exclusive scan of the pass histogram)
+    const uint32_t gstart = LB ? block_exclusive_scan((uint32_t)tid < ndig ? hist[tid] : 0u, wsum, &total) : 0u;
     if ((uint32_t)tid < ndig) {
         dbase[tid] = db;
         uint32_t o = db;
@@ -220,10 +299,25 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
             wcnt[w][tid] = o;
             o += c[w];
         }
+        if (LB) {
+            // this tile's offset inside digit tid: decoupled look-back over earlier tiles
+            uint64_t* col = status + tid;
+            uint32_t excl = 0;
+            if (t == 0) {
+                lb_store(col, LB_PRE | tot);
+            } else {
+                lb_store(col + (size_t)t * RADIX, LB_AGG | tot);
+                excl = lb_lookback(col, RADIX, t);
+                lb_store(col + (size_t)t * RADIX, LB_PRE | (excl + tot));
+            }
+            gbase[tid] = gstart + excl;
+        } else {
+            gbase[tid] = hist[(size_t)tid * gridDim.x + t];
+        }
     }
     __syncthreads();
 #pragma unroll
-    for (int r = 0; r < SORT_ITEMS; ++r) {
+    for (int r = 0; r < ITEMS; ++r) {
         const size_t idx = wbase + (size_t)r * 64 + lane;
         if (idx < n) {
             const uint32_t pos = wcnt[wid][(key[r] >> shift) & mask] + rk[r];
@@ -233,7 +327,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
         }
     }
     __syncthreads();
-    const int nvalid = (int)min((size_t)SORT_TILE, n - bbase);
+    const int nvalid = (int)min((size_t)TILE, n - bbase);
     for (int p = tid; p < nvalid; p += SORT_THREADS) {
         const uint32_t k = s_key[p];
         const uint32_t d = (k >> shift) & mask;
@@ -246,27 +340,55 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
 
 // ----------------------------------------------------------- duplicate ----
 // One thread per depth-ordered Gaussian: emit its tiles (y outer, x inner, as
-// rasterizer_impl.cu:98-108) into consecutive instance slots.
+// rasterizer_impl.cu:98-108) into consecutive instance slots.  A block's 256
+// consecutive depth-ordered Gaussians own one contiguous slot range; when it fits
+// in LDS the keys are assembled there and written out with consecutive threads on
+// consecutive slots (per-thread runs at scattered offsets would make every store
+// instruction touch 64 partial lines).  Oversized ranges are written directly.
+constexpr int DUP_CAP = 4096;
 __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __restrict__ order,
                                                    const uint32_t* __restrict__ offsets,
                                                    const uint32_t* __restrict__ tiles_touched,
                                                    const ushort4* __restrict__ rect, int gx,
                                                    uint32_t* __restrict__ tkeys, uint32_t* __restrict__ slot_gid,
                                                    uint32_t* __restrict__ goff) {
-    const int r = blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= P) return;
-    const uint32_t g = order[r];
-    const uint32_t cnt = tiles_touched[g];
-    if (cnt == 0) return;
-    uint32_t off = r == 0 ? 0u : offsets[r - 1];
-    goff[g] = off;
-    const ushort4 rc = rect[g];
-    for (int y = rc.y; y < rc.w; ++y)
-        for (int x = rc.x; x < rc.z; ++x) {
-            tkeys[off] = (uint32_t)(y * gx + x);
-            slot_gid[off] = g;
-            ++off;
+    __shared__ uint32_t s_key[DUP_CAP], s_gid[DUP_CAP];
+    const int r0 = blockIdx.x * blockDim.x;
+    const int r = r0 + threadIdx.x;
+    const int rl = min(r0 + (int)blockDim.x, P) - 1;
+    const uint32_t bbase = r0 == 0 ? 0u : offsets[r0 - 1];
+    const uint32_t bend = offsets[rl];
+    const bool staged = bend - bbase <= (uint32_t)DUP_CAP;
+    if (r < P) {
+        const uint32_t g = order[r];
+        const uint32_t cnt = tiles_touched[g];
+        if (cnt != 0) {
+            uint32_t off = r == 0 ? 0u : offsets[r - 1];
+            goff[g] = off;
+            const ushort4 rc = rect[g];
+            if (staged) {
+                uint32_t lo = off - bbase;
+                for (int y = rc.y; y < rc.w; ++y)
+                    for (int x = rc.x; x < rc.z; ++x, ++lo) {
+                        s_key[lo] = (uint32_t)(y * gx + x);
+                        s_gid[lo] = g;
+                    }
+            } else {
+                for (int y = rc.y; y < rc.w; ++y)
+                    for (int x = rc.x; x < rc.z; ++x, ++off) {
+                        tkeys[off] = (uint32_t)(y * gx + x);
+                        slot_gid[off] = g;
+                    }
+            }
         }
+    }
+    if (!staged) return;  // uniform per block
+    __syncthreads();
+    const int n = (int)(bend - bbase);
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        tkeys[bbase + i] = s_key[i];
+        slot_gid[bbase + i] = s_gid[i];
+    }
 }
 
 // Tile ranges [first, last+1) from the sorted tile keys (identifyTileRanges,
@@ -326,34 +448,55 @@ uint32_t higher_msb(uint32_t n) {
     return msb;
 }
 
-static void scan_exclusive_inplace(uint32_t* data, size_t n, uint32_t* parts, hipStream_t st) {
-    const size_t nb = cdiv(n, SCAN_TILE);
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_THREADS), 0, st, data, nullptr, n, parts);
-    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(SCAN_THREADS), 0, st, parts, nb);
-    hipLaunchKernelGGL(k_scan_down<false>, dim3(nb), dim3(SCAN_THREADS), 0, st, data, nullptr, n, parts, data);
-}
-
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
-                                  uint32_t* parts, hipStream_t st) {
+                                  void* ws, hipStream_t st) {
     if (n == 0) return;
-    const size_t nb = cdiv(n, SCAN_TILE);
-    hipLaunchKernelGGL(k_scan_reduce, dim3(nb), dim3(SCAN_THREADS), 0, st, src, gather_idx, n, parts);
-    hipLaunchKernelGGL(k_scan_parts, dim3(1), dim3(SCAN_THREADS), 0, st, parts, nb);
-    hipLaunchKernelGGL(k_scan_down<true>, dim3(nb), dim3(SCAN_THREADS), 0, st, src, gather_idx, n, parts, out);
+    const ScanWs W = scan_ws(n, ws);
+    (void)hipMemsetAsync(W.base, 0, W.bytes, st);
+    hipLaunchKernelGGL(k_scan<true>, dim3(cdiv(n, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, src, gather_idx, n, out,
+                       W.status, W.counter);
 }
 
-// Stable LSD sort of (keys, vals) on the low key_bits bits.  Ping-pongs between
-// (keys_tmp, vals_tmp) and (keys_out, vals_out); the result always lands in
-// (keys_out, vals_out).  keys_in/vals_in are not modified.
+// Sorting modes (measured on MI355X): small sorts are launch-bound and use one
+// look-back scatter launch per pass; large sorts are bandwidth-bound and use the
+// table-driven passes, whose per-pass histogram + scan launches cost less than the
+// look-back chain over thousands of tiles.
+#ifndef GSR_SORT_LB_MAX
+#define GSR_SORT_LB_MAX (4u << 20)
+#endif
+#ifndef GSR_LB_ITEMS
+#define GSR_LB_ITEMS 16
+#endif
+#ifndef GSR_TB_ITEMS
+#define GSR_TB_ITEMS 8
+#endif
+
+template <int ITEMS, bool LB>
+static void launch_scatter(size_t n, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
+                           int shift, int bits, const uint32_t* hist, uint64_t* status, uint32_t* counter,
+                           const uint32_t* v2in, uint32_t* v2out, hipStream_t st) {
+    hipLaunchKernelGGL((k_radix_scatter<ITEMS, LB>), dim3(sort_tiles(n, ITEMS)), dim3(SORT_THREADS), 0, st, kin,
+                       vin, kout, vout, n, shift, bits, hist, status, counter, v2in, v2out);
+}
+
+// Stable LSD sort of (keys, vals[, vals2]) on the low key_bits bits.  Ping-pongs
+// between the _tmp and _out arrays; the result always lands in the _out arrays.
+// keys_in / vals_in / vals2_in are not modified.
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_tmp, uint32_t* vals_tmp,
-                       uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits, uint32_t* hist,
-                       uint32_t* parts, hipStream_t st, const uint32_t* vals2_in, uint32_t* vals2_tmp,
-                       uint32_t* vals2_out) {
+                       uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits, void* ws, hipStream_t st,
+                       const uint32_t* vals2_in, uint32_t* vals2_tmp, uint32_t* vals2_out) {
     if (n == 0) return;
     if (key_bits < 1) key_bits = 1;
     const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
     const int per_pass = (key_bits + passes - 1) / passes;  // balanced: 13 bits -> 7 + 6
-    const size_t nb = sort_blocks(n);
+    const SortWs W = sort_ws(n, ws);
+    const bool lb = n <= GSR_SORT_LB_MAX;
+    if (lb) {
+        const size_t nt = sort_tiles(n, GSR_LB_ITEMS);
+        (void)hipMemsetAsync(W.base, 0, W.header + (size_t)passes * nt * RADIX * 8, st);
+        hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)min(nt, (size_t)1024)), dim3(SORT_THREADS), 0, st, keys_in,
+                           n, passes, per_pass, key_bits, W.hist);
+    }
     const uint32_t* kin = keys_in;
     const uint32_t* vin = vals_in;
     const uint32_t* v2in = vals2_in;
@@ -365,11 +508,22 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
         uint32_t* kout = to_out ? keys_out : keys_tmp;
         uint32_t* vout = to_out ? vals_out : vals_tmp;
         uint32_t* v2out = vals2_in ? (to_out ? vals2_out : vals2_tmp) : nullptr;
-        hipLaunchKernelGGL(k_radix_upsweep, dim3(nb), dim3(SORT_THREADS), 0, st, kin, n, shift,
-                           (1u << bits) - 1u, hist);
-        scan_exclusive_inplace(hist, ((size_t)1 << bits) * nb, parts, st);
-        hipLaunchKernelGGL(k_radix_scatter, dim3(nb), dim3(SORT_THREADS), 0, st, kin, vin, kout, vout, n, shift,
-                           bits, hist, v2in, v2out);
+        if (lb) {
+            const size_t nt = sort_tiles(n, GSR_LB_ITEMS);
+            launch_scatter<GSR_LB_ITEMS, true>(n, kin, vin, kout, vout, shift, bits, W.hist + p * RADIX,
+                                               W.status + (size_t)p * nt * RADIX, W.counter + p, v2in, v2out, st);
+        } else {
+            const size_t nt = sort_tiles(n, GSR_TB_ITEMS);
+            const size_t len = ((size_t)1 << bits) * nt;
+            hipLaunchKernelGGL(k_radix_upsweep<GSR_TB_ITEMS>, dim3(nt), dim3(SORT_THREADS), 0, st, kin, n, shift,
+                               bits, W.table);
+            const ScanWs S = scan_ws(len, W.scan);
+            (void)hipMemsetAsync(S.base, 0, S.bytes, st);
+            hipLaunchKernelGGL(k_scan<false>, dim3(cdiv(len, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, W.table,
+                               nullptr, len, W.table, S.status, S.counter);
+            launch_scatter<GSR_TB_ITEMS, false>(n, kin, vin, kout, vout, shift, bits, W.table, nullptr, nullptr,
+                                                v2in, v2out, st);
+        }
         kin = kout;
         vin = vout;
         v2in = v2out;

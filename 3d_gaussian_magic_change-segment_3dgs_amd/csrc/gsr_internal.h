@@ -27,13 +27,51 @@ inline size_t align_up(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
 inline size_t cdiv(size_t a, size_t b) { return (a + b - 1) / b; }
 
 inline size_t sort_blocks(size_t n) { return n ? cdiv(n, SORT_TILE) : 0; }
-inline size_t hist_len(size_t n) { return (size_t)RADIX * sort_blocks(n); }
-inline size_t scan_parts(size_t n) { return cdiv(n > 0 ? n : 1, SCAN_TILE) + 1; }
+constexpr int MAX_SORT_PASSES = 4;
+
+// Workspaces of the single-pass (decoupled look-back) scan and radix sort: tile
+// counters, pass histograms and per-tile status words, zeroed before each use.
+struct ScanWs {
+    void* base;
+    size_t bytes;
+    uint32_t* counter;
+    uint64_t* status;
+};
+inline size_t scan_ws_bytes(size_t n) { return ALIGN + cdiv(n > 0 ? n : 1, SCAN_TILE) * 8; }
+inline ScanWs scan_ws(size_t n, void* p) {
+    char* c = static_cast<char*>(p);
+    return {p, scan_ws_bytes(n), reinterpret_cast<uint32_t*>(c), reinterpret_cast<uint64_t*>(c + ALIGN)};
+}
+struct SortWs {
+    void* base;
+    size_t header;      // bytes of counter + pass histograms
+    uint32_t* counter;  // [passes] tile counters (look-back mode)
+    uint32_t* hist;     // [passes][RADIX] global digit histograms (look-back mode)
+    uint64_t* status;   // [passes][tiles][RADIX] look-back status words
+    uint32_t* table;    // [RADIX][tiles] per-tile histograms (table mode; aliases status)
+    void* scan;         // scan workspace of the table (table mode)
+};
+constexpr int MIN_SORT_ITEMS = 4;
+inline size_t sort_tiles(size_t n, int items) { return n ? cdiv(n, (size_t)SORT_THREADS * items) : 0; }
+inline size_t sort_ws_bytes(size_t n, int passes) {
+    const size_t nt = sort_tiles(n, MIN_SORT_ITEMS);
+    const size_t lb = (size_t)passes * nt * RADIX * 8;
+    const size_t tb = align_up(nt * RADIX * 4) + scan_ws_bytes(nt * RADIX);
+    return ALIGN + align_up((size_t)MAX_SORT_PASSES * RADIX * 4) + (lb > tb ? lb : tb);
+}
+inline SortWs sort_ws(size_t n, void* p) {
+    char* c = static_cast<char*>(p);
+    const size_t hdr = ALIGN + align_up((size_t)MAX_SORT_PASSES * RADIX * 4);
+    const size_t nt = sort_tiles(n, MIN_SORT_ITEMS);
+    return {p, hdr, reinterpret_cast<uint32_t*>(c), reinterpret_cast<uint32_t*>(c + ALIGN),
+            reinterpret_cast<uint64_t*>(c + hdr), reinterpret_cast<uint32_t*>(c + hdr),
+            c + hdr + align_up(nt * RADIX * 4)};
+}
 
 // ---- geometry buffer (reference GeometryState, rasterizer_impl.cu:155-171) ----
 struct GeomLayout {
-    size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, goff,
-        hist, parts, bytes;
+    size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, goff, ws,
+        bytes;
 };
 inline GeomLayout geom_layout(size_t P) {
     GeomLayout L{};
@@ -49,16 +87,15 @@ inline GeomLayout geom_layout(size_t P) {
     L.dkeys_alt = take(P * 4);
     L.offsets = take(P * 4);
     L.goff = take(P * 4);
-    size_t hl = hist_len(P);
-    L.hist = take(hl * 4);
-    L.parts = take(scan_parts(hl > P ? hl : P) * 4);
+    const size_t sw = sort_ws_bytes(P, MAX_SORT_PASSES), cw = scan_ws_bytes(P);
+    L.ws = take(sw > cw ? sw : cw);  // depth sort, then the scan
     L.bytes = o + ALIGN;
     return L;
 }
 
 // ---- binning buffer (reference BinningState, rasterizer_impl.cu:181-194) ----
 struct BinLayout {
-    size_t tkeys, tkeys_alt, vals_alt, slot_vals, slot_gid, gid_alt, point_list, hist, parts, bytes;
+    size_t tkeys, tkeys_alt, vals_alt, slot_vals, slot_gid, gid_alt, point_list, ws, bytes;
 };
 inline BinLayout bin_layout(size_t I) {
     BinLayout L{};
@@ -71,9 +108,7 @@ inline BinLayout bin_layout(size_t I) {
     L.slot_gid = take(I * 4);
     L.gid_alt = take(I * 4);
     L.point_list = take(I * 4);
-    size_t hl = hist_len(I);
-    L.hist = take(hl * 4);
-    L.parts = take(scan_parts(hl) * 4);
+    L.ws = take(sort_ws_bytes(I, MAX_SORT_PASSES));
     L.bytes = o + ALIGN;
     return L;
 }
@@ -129,11 +164,11 @@ void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const
 // binning.hip
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL = identity*/, uint32_t* keys_tmp,
                        uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,
-                       uint32_t* hist, uint32_t* parts, hipStream_t st, const uint32_t* vals2_in = nullptr,
-                       uint32_t* vals2_tmp = nullptr, uint32_t* vals2_out = nullptr);
+                       void* ws, hipStream_t st, const uint32_t* vals2_in = nullptr, uint32_t* vals2_tmp = nullptr,
+                       uint32_t* vals2_out = nullptr);
 void launch_tile_order(const uint2* ranges, int T, uint32_t* order, hipStream_t st);
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
-                                  uint32_t* parts, hipStream_t st);
+                                  void* ws, hipStream_t st);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, int gx, uint32_t* tkeys, uint32_t* slot_gid, uint32_t* goff,
                       hipStream_t st);
