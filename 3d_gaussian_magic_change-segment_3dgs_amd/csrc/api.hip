@@ -121,7 +121,7 @@ size_t gsr_geom_bytes(int P) { return gsr::geom_layout(P > 0 ? (size_t)P : 0).by
 size_t gsr_binning_bytes(int num_rendered) { return gsr::bin_layout(num_rendered > 0 ? (size_t)num_rendered : 0).bytes; }
 size_t gsr_img_bytes(int W, int H) { return gsr::img_layout(W, H).bytes; }
 size_t gsr_backward_scratch_bytes(int num_rendered) {
-    return gsr::scratch_layout(num_rendered > 0 ? (size_t)num_rendered : 0).bytes;
+    return gsr::scratch_bytes(num_rendered > 0 ? (size_t)num_rendered : 0);
 }
 
 int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* stream,
@@ -141,8 +141,11 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
     char* g = aligned_base(geom);
     {
         StageScope sc(GSR_STAGE_PREPROCESS, st);
+        const bool lb = sort_uses_lookback(P);
         launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
-                          at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect), st);
+                          at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect),
+                          g + L.ws, lb ? sort_lb_zero_bytes(P, depth_sort_passes(), sort_lb_items()) : 0,
+                          g + L.ws_scan, scan_ws_bytes(P), st);
     }
     GSR_STAGE("preprocess");
     {
@@ -150,13 +153,13 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
         StageScope sc(GSR_STAGE_DEPTH_SORT, st);
         launch_radix_sort(at<uint32_t>(g, L.depth_keys), nullptr, at<uint32_t>(g, L.dkeys_alt),
                           at<uint32_t>(g, L.order_alt), at<uint32_t>(g, L.depth_keys), at<uint32_t>(g, L.order), P,
-                          32, g + L.ws, st);
+                          32, g + L.ws, /*ws_zeroed=*/true, st);
     }
     GSR_STAGE("depth sort");
     {
         StageScope sc(GSR_STAGE_SCAN, st);
         launch_scan_inclusive_gather(at<uint32_t>(g, L.tiles_touched), at<uint32_t>(g, L.order),
-                                     at<uint32_t>(g, L.offsets), P, g + L.ws, st);
+                                     at<uint32_t>(g, L.offsets), P, g + L.ws_scan, /*ws_zeroed=*/true, st);
     }
     GSR_STAGE("scan");
     uint32_t total = 0;
@@ -184,7 +187,8 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
     const int T = IL.gx * IL.gy;
     char* im = aligned_base(img);
     uint2* ranges = at<uint2>(im, IL.ranges);
-    if (hipMemsetAsync(ranges, 0, (size_t)T * sizeof(uint2), st) != hipSuccess) return fail("[gsr] memset ranges");
+    if (I == 0 && hipMemsetAsync(ranges, 0, (size_t)T * sizeof(uint2), st) != hipSuccess)
+        return fail("[gsr] memset ranges");  // otherwise k_duplicate clears them
     const GeomLayout GL = geom_layout(P > 0 ? P : 0);
     char* g = P > 0 ? aligned_base(geom) : nullptr;
     const BinLayout BL = bin_layout(I);
@@ -196,7 +200,8 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
             StageScope sc(GSR_STAGE_DUPLICATE, st);
             launch_duplicate(P, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets),
                              at<uint32_t>(g, GL.tiles_touched), at<ushort4>(g, GL.rect), IL.gx,
-                             at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid), at<uint32_t>(g, GL.goff), st);
+                             at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid), at<uint32_t>(g, GL.goff),
+                             ranges, T, st);
         }
         GSR_STAGE("duplicate");
         const int bits = (int)higher_msb((uint32_t)T);
@@ -211,7 +216,7 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
             // (depth, gaussian); the id travels along so point_list needs no gather.
             StageScope sc(GSR_STAGE_TILE_SORT, st);
             launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout, at<uint32_t>(b, BL.slot_vals),
-                              I, bits, b + BL.ws, st,
+                              I, bits, b + BL.ws, /*ws_zeroed=*/false, st,
                               at<uint32_t>(b, BL.slot_gid), at<uint32_t>(b, BL.gid_alt),
                               at<uint32_t>(b, BL.point_list));
         }
@@ -219,7 +224,7 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
         point_list = at<uint32_t>(b, BL.point_list);
         {
             StageScope sc(GSR_STAGE_RANGES, st);
-            launch_finalize(I, kout, ranges, st);
+            launch_finalize(I, kout, ranges, at<uint32_t>(b, BL.written), st);
         }
         GSR_STAGE("tile ranges");
     }
@@ -260,14 +265,10 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
         if (!binning || !scratch) return fail("[gsr] binning/scratch buffer is NULL");
         const BinLayout BL = bin_layout(I);
         char* b = aligned_base(binning);
-        const ScratchLayout SL = scratch_layout(I);
-        char* sc0 = aligned_base(scratch);
-        contrib = reinterpret_cast<float*>(sc0 + SL.contrib);
-        written = reinterpret_cast<uint32_t*>(sc0 + SL.written);
+        contrib = reinterpret_cast<float*>(aligned_base(scratch));
+        written = at<uint32_t>(b, BL.written);  // cleared by the forward's k_finalize
         {
             StageScope sc(GSR_STAGE_RENDER_BWD, st);
-            if (hipMemsetAsync(written, 0, cdiv(I, 32) * 4, st) != hipSuccess)
-                return fail("[gsr] hipMemsetAsync failed");
             launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order), at<uint2>(im, IL.ranges),
                                    at<uint32_t>(b, BL.point_list), at<uint32_t>(b, BL.slot_vals),
                                    at<float4>(g, GL.rec), s->bg, alpha, at<uint32_t>(im, IL.n_contrib), dL_dcolor,

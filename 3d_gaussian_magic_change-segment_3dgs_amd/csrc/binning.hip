@@ -190,8 +190,10 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __r
 // so skewed digit distributions do not serialise on one LDS address.
 template <int ITEMS>
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_upsweep(const uint32_t* __restrict__ keys, size_t n,
-                                                                int shift, int bits, uint32_t* __restrict__ hist) {
+                                                                int shift, int bits, uint32_t* __restrict__ hist,
+                                                                void* scan_ws, size_t scan_ws16) {
     __shared__ uint32_t cnt[RADIX];
+    zero16(scan_ws, scan_ws16, (size_t)blockIdx.x * SORT_THREADS + threadIdx.x, (size_t)gridDim.x * SORT_THREADS);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t ndig = 1u << bits, mask = ndig - 1u;
     cnt[tid] = 0;
@@ -351,8 +353,11 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
                                                    const uint32_t* __restrict__ tiles_touched,
                                                    const ushort4* __restrict__ rect, int gx,
                                                    uint32_t* __restrict__ tkeys, uint32_t* __restrict__ slot_gid,
-                                                   uint32_t* __restrict__ goff) {
+                                                   uint32_t* __restrict__ goff, uint2* __restrict__ ranges, int T) {
     __shared__ uint32_t s_key[DUP_CAP], s_gid[DUP_CAP];
+    // empty tiles keep ranges {0, 0} (rasterizer_impl.cu:316 memset), set here
+    for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < T; i += gridDim.x * blockDim.x)
+        ranges[i] = make_uint2(0u, 0u);
     const int r0 = blockIdx.x * blockDim.x;
     const int r = r0 + threadIdx.x;
     const int rl = min(r0 + (int)blockDim.x, P) - 1;
@@ -394,8 +399,10 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
 // Tile ranges [first, last+1) from the sorted tile keys (identifyTileRanges,
 // rasterizer_impl.cu:113-138).
 __global__ void __launch_bounds__(256) k_finalize(size_t I, const uint32_t* __restrict__ tkeys,
-                                                  uint2* __restrict__ ranges) {
+                                                  uint2* __restrict__ ranges, uint32_t* __restrict__ written) {
     const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+    // the backward's written-slot mask starts empty
+    if (k < cdiv(I, 128)) reinterpret_cast<uint4*>(written)[k] = make_uint4(0u, 0u, 0u, 0u);
     if (k >= I) return;
     const uint32_t t = tkeys[k];
     if (k == 0 || tkeys[k - 1] != t) ranges[t].x = (uint32_t)k;
@@ -449,10 +456,10 @@ uint32_t higher_msb(uint32_t n) {
 }
 
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
-                                  void* ws, hipStream_t st) {
+                                  void* ws, bool ws_zeroed, hipStream_t st) {
     if (n == 0) return;
     const ScanWs W = scan_ws(n, ws);
-    (void)hipMemsetAsync(W.base, 0, W.bytes, st);
+    if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, W.bytes, st);
     hipLaunchKernelGGL(k_scan<true>, dim3(cdiv(n, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, src, gather_idx, n, out,
                        W.status, W.counter);
 }
@@ -471,6 +478,10 @@ void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_id
 #define GSR_TB_ITEMS 8
 #endif
 
+int depth_sort_passes() { return 4; }
+int sort_lb_items() { return GSR_LB_ITEMS; }
+bool sort_uses_lookback(size_t n) { return n <= GSR_SORT_LB_MAX; }
+
 template <int ITEMS, bool LB>
 static void launch_scatter(size_t n, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
                            int shift, int bits, const uint32_t* hist, uint64_t* status, uint32_t* counter,
@@ -483,8 +494,8 @@ static void launch_scatter(size_t n, const uint32_t* kin, const uint32_t* vin, u
 // between the _tmp and _out arrays; the result always lands in the _out arrays.
 // keys_in / vals_in / vals2_in are not modified.
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_tmp, uint32_t* vals_tmp,
-                       uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits, void* ws, hipStream_t st,
-                       const uint32_t* vals2_in, uint32_t* vals2_tmp, uint32_t* vals2_out) {
+                       uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits, void* ws, bool ws_zeroed,
+                       hipStream_t st, const uint32_t* vals2_in, uint32_t* vals2_tmp, uint32_t* vals2_out) {
     if (n == 0) return;
     if (key_bits < 1) key_bits = 1;
     const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
@@ -493,7 +504,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     const bool lb = n <= GSR_SORT_LB_MAX;
     if (lb) {
         const size_t nt = sort_tiles(n, GSR_LB_ITEMS);
-        (void)hipMemsetAsync(W.base, 0, W.header + (size_t)passes * nt * RADIX * 8, st);
+        if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, GSR_LB_ITEMS), st);
         hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)min(nt, (size_t)1024)), dim3(SORT_THREADS), 0, st, keys_in,
                            n, passes, per_pass, key_bits, W.hist);
     }
@@ -515,10 +526,9 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
         } else {
             const size_t nt = sort_tiles(n, GSR_TB_ITEMS);
             const size_t len = ((size_t)1 << bits) * nt;
-            hipLaunchKernelGGL(k_radix_upsweep<GSR_TB_ITEMS>, dim3(nt), dim3(SORT_THREADS), 0, st, kin, n, shift,
-                               bits, W.table);
             const ScanWs S = scan_ws(len, W.scan);
-            (void)hipMemsetAsync(S.base, 0, S.bytes, st);
+            hipLaunchKernelGGL(k_radix_upsweep<GSR_TB_ITEMS>, dim3(nt), dim3(SORT_THREADS), 0, st, kin, n, shift,
+                               bits, W.table, S.base, cdiv(S.bytes, 16));
             hipLaunchKernelGGL(k_scan<false>, dim3(cdiv(len, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, W.table,
                                nullptr, len, W.table, S.status, S.counter);
             launch_scatter<GSR_TB_ITEMS, false>(n, kin, vin, kout, vout, shift, bits, W.table, nullptr, nullptr,
@@ -537,15 +547,15 @@ void launch_tile_order(const uint2* ranges, int T, uint32_t* order, hipStream_t 
 
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, int gx, uint32_t* tkeys, uint32_t* slot_gid, uint32_t* goff,
-                      hipStream_t st) {
+                      uint2* ranges, int T, hipStream_t st) {
     if (P == 0) return;
     hipLaunchKernelGGL(k_duplicate, dim3(cdiv(P, 256)), dim3(256), 0, st, P, order, offsets, tiles_touched, rect,
-                       gx, tkeys, slot_gid, goff);
+                       gx, tkeys, slot_gid, goff, ranges, T);
 }
 
-void launch_finalize(size_t I, const uint32_t* tkeys, uint2* ranges, hipStream_t st) {
+void launch_finalize(size_t I, const uint32_t* tkeys, uint2* ranges, uint32_t* written, hipStream_t st) {
     if (I == 0) return;
-    hipLaunchKernelGGL(k_finalize, dim3(cdiv(I, 256)), dim3(256), 0, st, I, tkeys, ranges);
+    hipLaunchKernelGGL(k_finalize, dim3(cdiv(I, 256)), dim3(256), 0, st, I, tkeys, ranges, written);
 }
 
 }  // namespace gsr

@@ -24,7 +24,14 @@ constexpr int RADIX_BITS = 8, RADIX = 1 << RADIX_BITS;
 
 constexpr size_t ALIGN = 256;
 inline size_t align_up(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
-inline size_t cdiv(size_t a, size_t b) { return (a + b - 1) / b; }
+__host__ __device__ inline size_t cdiv(size_t a, size_t b) { return (a + b - 1) / b; }
+
+// Zero n4 16-B words with a grid-stride loop: lets a kernel that runs anyway clear
+// the next stage's counters instead of a separate memset launch.
+__device__ __forceinline__ void zero16(void* p, size_t n4, size_t tid, size_t nthreads) {
+    uint4* q = static_cast<uint4*>(p);
+    for (size_t i = tid; i < n4; i += nthreads) q[i] = make_uint4(0u, 0u, 0u, 0u);
+}
 
 inline size_t sort_blocks(size_t n) { return n ? cdiv(n, SORT_TILE) : 0; }
 constexpr int MAX_SORT_PASSES = 4;
@@ -59,6 +66,10 @@ inline size_t sort_ws_bytes(size_t n, int passes) {
     const size_t tb = align_up(nt * RADIX * 4) + scan_ws_bytes(nt * RADIX);
     return ALIGN + align_up((size_t)MAX_SORT_PASSES * RADIX * 4) + (lb > tb ? lb : tb);
 }
+// Bytes of the workspace a look-back sort of n keys in `passes` passes needs zeroed.
+inline size_t sort_lb_zero_bytes(size_t n, int passes, int items) {
+    return ALIGN + align_up((size_t)MAX_SORT_PASSES * RADIX * 4) + (size_t)passes * sort_tiles(n, items) * RADIX * 8;
+}
 inline SortWs sort_ws(size_t n, void* p) {
     char* c = static_cast<char*>(p);
     const size_t hdr = ALIGN + align_up((size_t)MAX_SORT_PASSES * RADIX * 4);
@@ -71,7 +82,7 @@ inline SortWs sort_ws(size_t n, void* p) {
 // ---- geometry buffer (reference GeometryState, rasterizer_impl.cu:155-171) ----
 struct GeomLayout {
     size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, goff, ws,
-        bytes;
+        ws_scan, bytes;
 };
 inline GeomLayout geom_layout(size_t P) {
     GeomLayout L{};
@@ -87,15 +98,15 @@ inline GeomLayout geom_layout(size_t P) {
     L.dkeys_alt = take(P * 4);
     L.offsets = take(P * 4);
     L.goff = take(P * 4);
-    const size_t sw = sort_ws_bytes(P, MAX_SORT_PASSES), cw = scan_ws_bytes(P);
-    L.ws = take(sw > cw ? sw : cw);  // depth sort, then the scan
+    L.ws = take(sort_ws_bytes(P, MAX_SORT_PASSES));  // depth sort
+    L.ws_scan = take(scan_ws_bytes(P));              // tiles_touched scan
     L.bytes = o + ALIGN;
     return L;
 }
 
 // ---- binning buffer (reference BinningState, rasterizer_impl.cu:181-194) ----
 struct BinLayout {
-    size_t tkeys, tkeys_alt, vals_alt, slot_vals, slot_gid, gid_alt, point_list, ws, bytes;
+    size_t tkeys, tkeys_alt, vals_alt, slot_vals, slot_gid, gid_alt, point_list, written, ws, bytes;
 };
 inline BinLayout bin_layout(size_t I) {
     BinLayout L{};
@@ -108,24 +119,14 @@ inline BinLayout bin_layout(size_t I) {
     L.slot_gid = take(I * 4);
     L.gid_alt = take(I * 4);
     L.point_list = take(I * 4);
+    L.written = take(cdiv(I, 128) * 16);  // backward: 1 bit per instance slot (zeroed by k_finalize)
     L.ws = take(sort_ws_bytes(I, MAX_SORT_PASSES));
     L.bytes = o + ALIGN;
     return L;
 }
 
-// ---- backward scratch: per-instance gradient records + written-slot mask ----
-struct ScratchLayout {
-    size_t contrib, written, bytes;
-};
-inline ScratchLayout scratch_layout(size_t I) {
-    ScratchLayout L{};
-    size_t o = 0;
-    auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes); return r; };
-    L.contrib = take(I * 12 * sizeof(float));
-    L.written = take(cdiv(I, 32) * 4);
-    L.bytes = o + ALIGN;
-    return L;
-}
+// ---- backward scratch: per-instance gradient records ----
+inline size_t scratch_bytes(size_t I) { return align_up(I * 12 * sizeof(float)) + ALIGN; }
 
 // ---- image buffer (reference ImageState, rasterizer_impl.cu:173-179) ----
 struct ImgLayout {
@@ -155,7 +156,8 @@ inline char* aligned_base(void* p) {
 // preprocess.hip
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec,
                        int* radii, uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped,
-                       ushort4* rect, hipStream_t st);
+                       ushort4* rect, void* zero_a, size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes,
+                       hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
@@ -164,15 +166,18 @@ void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const
 // binning.hip
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL = identity*/, uint32_t* keys_tmp,
                        uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,
-                       void* ws, hipStream_t st, const uint32_t* vals2_in = nullptr, uint32_t* vals2_tmp = nullptr,
-                       uint32_t* vals2_out = nullptr);
+                       void* ws, bool ws_zeroed, hipStream_t st, const uint32_t* vals2_in = nullptr,
+                       uint32_t* vals2_tmp = nullptr, uint32_t* vals2_out = nullptr);
+int depth_sort_passes();
+int sort_lb_items();
+bool sort_uses_lookback(size_t n);
 void launch_tile_order(const uint2* ranges, int T, uint32_t* order, hipStream_t st);
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
-                                  void* ws, hipStream_t st);
+                                  void* ws, bool ws_zeroed, hipStream_t st);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, int gx, uint32_t* tkeys, uint32_t* slot_gid, uint32_t* goff,
-                      hipStream_t st);
-void launch_finalize(size_t I, const uint32_t* tkeys, uint2* ranges, hipStream_t st);
+                      uint2* ranges, int T, hipStream_t st);
+void launch_finalize(size_t I, const uint32_t* tkeys, uint2* ranges, uint32_t* written, hipStream_t st);
 // render.hip
 void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
                            const uint32_t* point_list,

@@ -202,8 +202,12 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
                                                     float4* __restrict__ rec, int* __restrict__ radii,
                                                     uint32_t* __restrict__ tiles_touched,
                                                     uint32_t* __restrict__ depth_keys,
-                                                    uint8_t* __restrict__ clamped, ushort4* __restrict__ rect) {
+                                                    uint8_t* __restrict__ clamped, ushort4* __restrict__ rect,
+                                                    void* zero_a, size_t zero_a16, void* zero_b, size_t zero_b16) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    // clear the depth sort's and the scan's look-back counters (saves two memset launches)
+    zero16(zero_a, zero_a16, idx, (size_t)gridDim.x * blockDim.x);
+    zero16(zero_b, zero_b16, idx, (size_t)gridDim.x * blockDim.x);
     if (idx >= s.P) return;
     Cam cam;
     load_cam(s, cam);
@@ -593,11 +597,12 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
 }  // namespace
 
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec, int* radii,
-                       uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped, ushort4* rect,
-                       hipStream_t st) {
+                       uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped, ushort4* rect, void* zero_a,
+                       size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_preprocess, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, gx, gy, rec, radii,
-                       tiles_touched, depth_keys, clamped, rect);
+                       tiles_touched, depth_keys, clamped, rect, zero_a, cdiv(zero_a_bytes, 16), zero_b,
+                       cdiv(zero_b_bytes, 16));
 }
 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {

@@ -205,15 +205,17 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
         geom = torch.empty(_lib.gsr_geom_bytes(P), **u8)
         img = torch.empty(_lib.gsr_img_bytes(W, H), **u8)
         radii = torch.empty(P, dtype=torch.int32, device=device)
+        # outputs are allocated before the num_rendered sync so that only the binning
+        # buffer is allocated between the sync and the render launches
+        color = torch.empty(NUM_CHANNELS, H, W, **f32)
+        depth = torch.empty(1, H, W, **f32)
+        alpha = torch.empty(1, H, W, **f32)
+        segment = torch.empty(NUM_CLASS, H, W, **f32)
         nr = ctypes.c_int(0)
         _check(_lib.gsr_forward_geometry(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), radii.data_ptr(),
                                          stream, ctypes.byref(nr)))
         num_rendered = int(nr.value)
         binning = torch.empty(_lib.gsr_binning_bytes(num_rendered), **u8)
-        color = torch.empty(NUM_CHANNELS, H, W, **f32)
-        depth = torch.empty(1, H, W, **f32)
-        alpha = torch.empty(1, H, W, **f32)
-        segment = torch.empty(NUM_CLASS, H, W, **f32)
         _check(_lib.gsr_forward_render(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), binning.data_ptr(),
                                        img.data_ptr(), num_rendered, color.data_ptr(), depth.data_ptr(),
                                        alpha.data_ptr(), segment.data_ptr(), stream))

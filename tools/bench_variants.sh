@@ -2,6 +2,7 @@
 # Bench every build/variants/libgsr_*.so (stage table) after the default build.
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
+shopt -s nullglob
 for so in "" build/variants/libgsr_*.so; do
   name=${so:-default}
   if [ -n "$so" ]; then export GSR_LIBRARY=$PWD/$so; else unset GSR_LIBRARY; fi
