@@ -100,13 +100,6 @@ extern "C" __attribute__((visibility("default"))) int gsr_stats_read(unsigned lo
 namespace gsr {
 namespace {
 
-__device__ __forceinline__ float bcast(float v, int j) {
-    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j));
-}
-__device__ __forceinline__ uint32_t bcast_u(uint32_t v, int j) {
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, j);
-}
-
 constexpr float ALPHA_MIN = 1.0f / 255.0f;  // forward.cu:352
 constexpr float T_MIN = 0.0001f;            // forward.cu:355
 constexpr float POWER_GUARD = 1e-3f;        // skip guard in ln-space (alpha factor e^-0.001)
@@ -202,6 +195,10 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     // Two-stage software pipeline over batches of 64 instances: while batch b is
     // blended, the records of batch b+1 and the ids of batch b+2 are in flight
     // (the id -> record dependency would otherwise stall every batch start).
+    // The batch's records are parked in LDS and read back with a wave-uniform address
+    // (a broadcast ds_read): the blend loop then spends no VALU issue slots on
+    // v_readlane broadcasts.  One wave per block, so the barriers are free.
+    __shared__ float4 srec[64][4];
     uint32_t g_next = lane < n ? point_list[range.x + lane] : 0u;
     Batch cur = fetch_batch(rec, g_next, lane < n);
     g_next = 64 + lane < n ? point_list[range.x + 64 + lane] : 0u;
@@ -216,11 +213,17 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
         const float pmin = power_floor(rb.y);
         uint64_t todo = __ballot(lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1));
         STAT(2, cnt - __popcll(todo));
+        __syncthreads();  // previous batch's reads are done
+        srec[lane][0] = ra;                                      // x, y, conic a, b
+        srec[lane][1] = make_float4(rb.x, pmin, rb.y, rb.w);     // conic c, power floor, opacity, seg0
+        srec[lane][2] = rc;                                      // r, g, b, seg1
+        srec[lane][3] = make_float4(rb.z, 0.f, 0.f, 0.f);        // depth
+        __syncthreads();
         while (todo) {
             const int j = (int)__builtin_ctzll(todo);
             todo &= todo - 1;
-            const float gx_ = bcast(ra.x, j), gy_ = bcast(ra.y, j);
-            const float ca = bcast(ra.z, j), cb = bcast(ra.w, j), cc = bcast(rb.x, j), pm = bcast(pmin, j);
+            const float4 q0 = srec[j][0], q1 = srec[j][1];
+            const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
             float power[4];
             bool near[4];
             const float dx = gx_ - pfx;
@@ -237,8 +240,9 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
                 continue;
             }
             STAT(3, 1);
-            const float op = bcast(rb.y, j), dep = bcast(rb.z, j), s0 = bcast(rb.w, j);
-            const float cr = bcast(rc.x, j), cg = bcast(rc.y, j), cbl = bcast(rc.z, j), s1 = bcast(rc.w, j);
+            const float4 q2 = srec[j][2], q3 = srec[j][3];
+            const float op = q1.z, dep = q3.x, s0 = q1.w;
+            const float cr = q2.x, cg = q2.y, cbl = q2.z, s1 = q2.w;
             const uint32_t contributor = (uint32_t)(base + j + 1);
             // Strip k (rows 4k..4k+3 of the tile) is blended only if one of its pixels
             // can pass; the exact reference tests below decide per pixel.
@@ -412,8 +416,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     STAT_DECL
     STAT(7, n);
     STAT(6, n > (int)maxlast ? n - (int)maxlast : 0);
-    // Same two-stage batch pipeline as the forward, walking the list back to front:
-    // lane l of the batch with upper end `top` owns position top-1-l.
+    // Same two-stage batch pipeline and LDS record broadcast as the forward, walking
+    // the list back to front: lane l of the batch with upper end `top` owns position top-1-l.
+    __shared__ float4 srec[64][4];
     const int top0 = (int)maxlast;
     bool v_next = lane < top0;
     uint32_t g_next = v_next ? point_list[range.x + (uint32_t)(top0 - 1 - lane)] : 0u;
@@ -439,14 +444,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
         const bool hit = lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1);
         uint64_t todo = __ballot(hit);
         STAT(2, cnt - __popcll(todo));
+        __syncthreads();  // previous batch's reads are done
+        srec[lane][0] = ra;                                                   // x, y, conic a, b
+        srec[lane][1] = make_float4(rb.x, pmin, rb.y, rb.w);                  // conic c, power floor, opacity, seg0
+        srec[lane][2] = rc;                                                   // r, g, b, seg1
+        srec[lane][3] = make_float4(rb.z, __uint_as_float(uslot), 0.f, 0.f);  // depth, record slot
+        __syncthreads();
         while (todo) {
             const int j = (int)__builtin_ctzll(todo);
             todo &= todo - 1;
             const uint32_t p = (uint32_t)(top - 1 - j);
-            const uint32_t u = bcast_u(uslot, j);
-            float* dst = contrib + (size_t)u * 12;
-            const float gx_ = bcast(ra.x, j), gy_ = bcast(ra.y, j);
-            const float ca = bcast(ra.z, j), cb = bcast(ra.w, j), cc = bcast(rb.x, j), pm = bcast(pmin, j);
+            const float4 q0 = srec[j][0], q1 = srec[j][1];
+            const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
             float power[4], dys[4];
             bool near[4];
             const float dx = gx_ - pfx;
@@ -464,8 +473,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                 continue;
             }
             STAT(3, 1);
-            const float op = bcast(rb.y, j), dep = bcast(rb.z, j), s0 = bcast(rb.w, j);
-            const float c0 = bcast(rc.x, j), c1 = bcast(rc.y, j), c2 = bcast(rc.z, j), s1 = bcast(rc.w, j);
+            const float4 q2 = srec[j][2], q3 = srec[j][3];
+            const float op = q1.z, dep = q3.x, s0 = q1.w;
+            const float c0 = q2.x, c1 = q2.y, c2 = q2.z, s1 = q2.w;
+            const uint32_t u = __float_as_uint(q3.y);
+            float* dst = contrib + (size_t)u * 12;
             float acc[12];
 #pragma unroll
             for (int i = 0; i < 12; ++i) acc[i] = 0.f;
