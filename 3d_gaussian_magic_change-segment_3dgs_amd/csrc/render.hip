@@ -112,20 +112,17 @@ __device__ __forceinline__ float power_floor(float opacity) {
     return -__logf(255.0f * opacity) - POWER_GUARD;
 }
 
-// Batch fetch: lane l loads the 48 B of instance (first + l) of the tile list.
+// Batch fetch: lane l loads the 48 B of one instance's record.  Loads are issued
+// unconditionally (callers clamp list positions into the tile's list, so g is always
+// a valid id): with no branch around them the number of loads in flight is static
+// and the waitcnt before the current batch's first use leaves the prefetched batch
+// in flight (a predicated load makes the compiler fall back to vmcnt(0)).
 struct Batch {
     float4 a, b, c;
 };
-__device__ __forceinline__ Batch fetch_batch(const float4* __restrict__ rec, uint32_t g, bool valid) {
-    Batch r;
-    r.a = r.b = r.c = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (valid) {
-        const float4* R = rec + (size_t)g * REC_F4;
-        r.a = R[0];
-        r.b = R[1];
-        r.c = R[2];
-    }
-    return r;
+__device__ __forceinline__ Batch fetch_batch(const float4* __restrict__ rec, uint32_t g) {
+    const float4* R = rec + (size_t)g * REC_F4;
+    return Batch{R[0], R[1], R[2]};
 }
 
 // Lane-parallel batch prefilter: can ANY pixel centre of the tile rectangle
@@ -199,15 +196,18 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     // (a broadcast ds_read): the blend loop then spends no VALU issue slots on
     // v_readlane broadcasts.  One wave per block, so the barriers are free.
     __shared__ float4 srec[64][4];
-    uint32_t g_next = lane < n ? point_list[range.x + lane] : 0u;
-    Batch cur = fetch_batch(rec, g_next, lane < n);
-    g_next = 64 + lane < n ? point_list[range.x + 64 + lane] : 0u;
+    const uint32_t* plist = point_list + range.x;
+    const int nlast = max(n - 1, 0);  // list positions are clamped to the last one
+    uint32_t g_next = n > 0 ? plist[min(lane, nlast)] : 0u;
+    Batch cur;
+    if (n > 0) cur = fetch_batch(rec, g_next);
+    if (n > 0) g_next = plist[min(64 + lane, nlast)];
     for (int base = 0; base < n; base += 64) {
         if (!__any((T[0] > 0.f) | (T[1] > 0.f) | (T[2] > 0.f) | (T[3] > 0.f))) break;
         const int cnt = min(64, n - base);
         STAT(5, 1);
-        const Batch nxt = fetch_batch(rec, g_next, base + 64 + lane < n);
-        g_next = base + 128 + lane < n ? point_list[range.x + base + 128 + lane] : 0u;
+        const Batch nxt = fetch_batch(rec, g_next);
+        g_next = plist[min(base + 128 + lane, nlast)];
         const float4 ra = cur.a, rb = cur.b, rc = cur.c;
         cur = nxt;
         const float pmin = power_floor(rb.y);
@@ -420,22 +420,28 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     // the list back to front: lane l of the batch with upper end `top` owns position top-1-l.
     __shared__ float4 srec[64][4];
     const int top0 = (int)maxlast;
-    bool v_next = lane < top0;
-    uint32_t g_next = v_next ? point_list[range.x + (uint32_t)(top0 - 1 - lane)] : 0u;
-    uint32_t u_next = v_next ? slot_vals[range.x + (uint32_t)(top0 - 1 - lane)] : 0u;
-    Batch cur = fetch_batch(rec, g_next, v_next);
+    const uint32_t* plist = point_list + range.x;
+    const uint32_t* slist = slot_vals + range.x;
+    // list positions below 0 are clamped to 0 (unconditional loads, see fetch_batch)
+    uint32_t g_next = 0u, u_next = 0u;
+    Batch cur;
+    if (top0 > 0) {
+        g_next = plist[max(top0 - 1 - lane, 0)];
+        u_next = slist[max(top0 - 1 - lane, 0)];
+        cur = fetch_batch(rec, g_next);
+    }
     uint32_t u_cur = u_next;
-    v_next = 64 + lane < top0;
-    g_next = v_next ? point_list[range.x + (uint32_t)(top0 - 65 - lane)] : 0u;
-    u_next = v_next ? slot_vals[range.x + (uint32_t)(top0 - 65 - lane)] : 0u;
+    if (top0 > 0) {
+        g_next = plist[max(top0 - 65 - lane, 0)];
+        u_next = slist[max(top0 - 65 - lane, 0)];
+    }
     for (int top = top0; top > 0; top -= 64) {
         const int cnt = min(64, top);
         STAT(5, 1);
-        const Batch nxt = fetch_batch(rec, g_next, v_next);
+        const Batch nxt = fetch_batch(rec, g_next);
         const uint32_t u_nxt = u_next;
-        v_next = 128 + lane < top;
-        g_next = v_next ? point_list[range.x + (uint32_t)(top - 129 - lane)] : 0u;
-        u_next = v_next ? slot_vals[range.x + (uint32_t)(top - 129 - lane)] : 0u;
+        g_next = plist[max(top - 129 - lane, 0)];
+        u_next = slist[max(top - 129 - lane, 0)];
         const float4 ra = cur.a, rb = cur.b, rc = cur.c;
         const uint32_t uslot = u_cur;
         cur = nxt;
