@@ -17,7 +17,7 @@ const char* const STAGE_NAMES[NUM_STAGES] = {"preprocess", "depth_sort", "scan",
                                              "ranges",     "render_fwd", "render_bwd", "gaussian_bwd"};
 struct Timer {
     std::mutex mu;
-    bool on = false;
+    unsigned mask = 0;  // bit i: time stage i
     struct Rec { int stage; hipEvent_t a, b; };
     std::vector<Rec> pending;
     std::vector<hipEvent_t> pool;
@@ -27,8 +27,10 @@ struct Timer {
             pool.pop_back();
             return e;
         }
+        // no system-scope fence on record: a fenced event costs ~10 us of pipeline
+        // drain between the kernels it separates
         hipEvent_t e = nullptr;
-        if (hipEventCreate(&e) != hipSuccess) e = nullptr;
+        if (hipEventCreateWithFlags(&e, hipEventDisableSystemFence) != hipSuccess) e = nullptr;
         return e;
     }
 };
@@ -43,7 +45,7 @@ struct StageScope {
     StageScope(int s, hipStream_t stream) : stage(s), st(stream) {
         Timer& T = timer();
         std::lock_guard<std::mutex> lk(T.mu);
-        if (!T.on) return;
+        if (!((T.mask >> stage) & 1u)) return;
         a = T.get();
         if (a && hipEventRecord(a, st) != hipSuccess) {
             T.pool.push_back(a);
@@ -289,10 +291,10 @@ int gsr_num_stages(void) { return NUM_STAGES; }
 
 const char* gsr_stage_name(int stage) { return (stage >= 0 && stage < NUM_STAGES) ? STAGE_NAMES[stage] : ""; }
 
-void gsr_timing_enable(int on) {
+void gsr_timing_enable(int stage_mask) {
     Timer& T = timer();
     std::lock_guard<std::mutex> lk(T.mu);
-    T.on = on != 0;
+    T.mask = (unsigned)stage_mask;
 }
 
 int gsr_timing_collect(double* ms, long long* counts) {

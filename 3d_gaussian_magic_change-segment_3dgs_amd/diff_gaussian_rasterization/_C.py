@@ -247,7 +247,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, segments, s
     Returns (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
     dL_drotations, dL_dsegments); gradients of absent (empty) inputs are None."""
     P = int(means3D.size(0))
-    H, W = int(dL_dout_color.size(1)), int(dL_dout_color.size(2))
+    shaped = next(t for t in (dL_dout_color, dL_dout_segment, dL_dout_depth, dL_dout_alpha, alpha) if t is not None)
+    H, W = int(shaped.size(-2)), int(shaped.size(-1))
     device = means3D.device
     with torch.cuda.device(device):
         means3D_ = _dev_f32(means3D, device, "means3D")
@@ -280,7 +281,8 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, segments, s
         inp = _inputs(means3D_, sh_, colors_, segments_, None, scales_, rotations_, cov_)  # opacities unused
         ups = [_dev_f32(t, device, n) for t, n in ((dL_dout_color, "dL_dcolor"), (dL_dout_segment, "dL_dsegment"),
                                                    (dL_dout_depth, "dL_ddepth"), (dL_dout_alpha, "dL_dalpha"))]
-        ups = [u if u is not None else torch.zeros(1, H, W, dtype=torch.float32, device=device) for u in ups]
+        ups = [u if u is not None else torch.zeros(c, H, W, dtype=torch.float32, device=device)
+               for u, c in zip(ups, (NUM_CHANNELS, NUM_CLASS, 1, 1))]
         alpha_ = _dev_f32(alpha, device, "alpha")
         radii_ = radii.contiguous()
         R = int(R)

@@ -92,6 +92,9 @@ class _RasterizeGaussians(torch.autograd.Function):
         ctx.save_for_backward(colors_precomp, segments, means3D, scales, rotations, cov3Ds_precomp, radii, sh,
                               geomBuffer, binningBuffer, imgBuffer, alpha)
         ctx.mark_non_differentiable(radii)
+        # No zero-filled stand-ins for outputs without a gradient (radii, or an image the
+        # loss does not use): the backward reads a missing image gradient as zeros.
+        ctx.set_materialize_grads(False)
         return color, radii, depth, alpha, segment
 
     @staticmethod

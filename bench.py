@@ -155,12 +155,27 @@ def main():
     torch.cuda.synchronize()
     nst = _C._lib.gsr_num_stages()
     import ctypes
-    ms = (ctypes.c_double * nst)()
-    cnt = (ctypes.c_longlong * nst)()
-    _C._lib.gsr_timing_collect(ms, cnt)  # drop warm-up events (timing off: no-op)
-    ms = (ctypes.c_double * nst)()
-    cnt = (ctypes.c_longlong * nst)()
-    _C._lib.gsr_timing_enable(1)
+    names = [_C._lib.gsr_stage_name(i).decode() for i in range(nst)]
+
+    def collect():
+        ms = (ctypes.c_double * nst)()
+        cnt = (ctypes.c_longlong * nst)()
+        _C._lib.gsr_timing_collect(ms, cnt)
+        return ms, cnt
+
+    collect()  # drop anything pending
+    # Stage pass (untimed): every stage bracketed by events -> the stage table and the
+    # dominant stage.  The brackets cost a few microseconds each, so the timed region
+    # below records events around the dominant stage only.
+    n_stage_steps = max(1, min(args.steps, 20))
+    _C._lib.gsr_timing_enable(-1)
+    for _ in range(n_stage_steps):
+        step()
+    torch.cuda.synchronize()
+    _C._lib.gsr_timing_enable(0)
+    sms, scnt = collect()
+    dom_i = max(range(nst), key=lambda i: sms[i]) if any(scnt) else 0
+    _C._lib.gsr_timing_enable(1 << dom_i)
     if dist is not None:
         dist.barrier()
     torch.cuda.synchronize()
@@ -172,27 +187,25 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     _C._lib.gsr_timing_enable(0)
-    _C._lib.gsr_timing_collect(ms, cnt)
+    ms, cnt = collect()  # the dominant stage's launches inside the timed region
     if dist is not None:
         t = torch.tensor([elapsed], device=device, dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-
     I, HW = int(state["I"]), W * H
     stages = {}
     for i in range(nst):
-        name = _C._lib.gsr_stage_name(i).decode()
-        if cnt[i]:
-            avg = ms[i] / cnt[i]
-            launches_per_step = cnt[i] / args.steps
-            stages[name] = {"avg_ms": round(avg, 4), "ms_per_step": round(ms[i] / args.steps, 4),
-                            "launches_per_step": launches_per_step,
-                            "gbs": round(algorithmic_bytes(name, P, I, HW, deg) / (avg * 1e-3) / 1e9, 1)}
-    dom = max(stages, key=lambda k: stages[k]["ms_per_step"]) if stages else None
+        if scnt[i]:
+            avg = sms[i] / scnt[i]
+            stages[names[i]] = {"avg_ms": round(avg, 4), "ms_per_step": round(sms[i] / n_stage_steps, 4),
+                                "launches_per_step": scnt[i] / n_stage_steps,
+                                "gbs": round(algorithmic_bytes(names[i], P, I, HW, deg) / (avg * 1e-3) / 1e9, 1)}
+    dom = names[dom_i] if stages else None
     value = world * args.steps / elapsed
     roof = None
-    if dom:
-        achieved = stages[dom]["gbs"]
+    if dom and cnt[dom_i]:
+        avg_live = ms[dom_i] / cnt[dom_i]  # measured inside the timed region
+        achieved = round(algorithmic_bytes(dom, P, I, HW, deg) / (avg_live * 1e-3) / 1e9, 1)
         traffic = valu_frac = None
         if os.path.exists(PMC_SUMMARY):
             try:
@@ -200,13 +213,13 @@ def main():
                 traffic = pk.get("hbm_bytes_per_launch")
                 if pk.get("SQ_INSTS_VALU"):
                     # wave64 VALU issue = 4 cycles on one of 1024 SIMDs, at the 2.4 GHz peak clock
-                    valu_frac = round(pk["SQ_INSTS_VALU"] * 4 / 1024 / (SIMD_CLOCK_HZ * stages[dom]["avg_ms"] * 1e-3), 4)
+                    valu_frac = round(pk["SQ_INSTS_VALU"] * 4 / 1024 / (SIMD_CLOCK_HZ * avg_live * 1e-3), 4)
             except Exception:
                 traffic = valu_frac = None
         roof = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg),
-                "avg_launch_ms": stages[dom]["avg_ms"],
+                "avg_launch_ms": round(avg_live, 4), "launches_timed": int(cnt[dom_i]),
                 "valu_issue_frac": valu_frac,
                 "whole_view_frac": round(view_bytes(P, I, HW, deg) * value / world / 1e9 / HBM_PEAK_GBS, 4)}
     out = {

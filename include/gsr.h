@@ -144,9 +144,11 @@ GSR_API int gsr_mark_visible(int P, const float* means3D, const float* viewmatri
 GSR_API long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered, void* geom,
                                  void* binning, void* img, void* dst, void* stream);
 
-/* ---- live stage timing (bench/profiling): when enabled, every stage of the
- * calls above is bracketed by hipEvents recorded on the caller's stream; no host
- * synchronisation is added.  gsr_timing_collect() waits for the recorded events,
+/* ---- live stage timing (bench/profiling): gsr_timing_enable(mask) brackets every
+ * stage i with (mask >> i) & 1 set (mask -1 = all, 0 = off) by hipEvents recorded
+ * on the caller's stream; no host synchronisation is added.  Each bracket costs a
+ * few microseconds of stream time, so time only the stages needed.
+ * gsr_timing_collect() waits for the recorded events,
  * accumulates per-stage milliseconds and launch counts into ms[i] / counts[i]
  * (arrays of gsr_num_stages() entries), and clears the pending list. */
 #define GSR_STAGE_PREPROCESS 0
@@ -160,7 +162,7 @@ GSR_API long long gsr_debug_copy(const char* name, int P, int W, int H, int num_
 #define GSR_STAGE_GAUSSIAN_BWD 8
 GSR_API int gsr_num_stages(void);
 GSR_API const char* gsr_stage_name(int stage);
-GSR_API void gsr_timing_enable(int on);
+GSR_API void gsr_timing_enable(int stage_mask);
 GSR_API int gsr_timing_collect(double* ms, long long* counts);
 
 /* Thread-local message of the last failing call ("" if none). */

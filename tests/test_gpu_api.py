@@ -110,3 +110,29 @@ def test_native_library_is_in_tree(gpu_available):
     assert os.path.realpath(_C.LIB_PATH).startswith(os.path.realpath(root))
     maps = open("/proc/self/maps").read()
     assert os.path.realpath(_C.LIB_PATH) in maps
+
+
+def test_loss_on_colour_only(gpu_available):
+    """Images the loss does not use get no gradient (None in backward): gsr reads them
+    as zeros, so the result equals passing explicit zero upstream gradients."""
+    from diff_gaussian_rasterization import _RasterizeGaussians
+    scene = synthetic_scene(4000, sh_degree=2, seed=23)
+    cam = orbit_camera(5, 128, 96, 140.0)
+    st = Hn.settings_for(cam, scene.sh_degree, "cuda")
+    E = torch.Tensor([])
+
+    def run(explicit_zeros):
+        leaf = lambda t: t.detach().to("cuda").clone().requires_grad_(True)
+        ins = [leaf(scene.means3D), torch.zeros(scene.P, 3, device="cuda", requires_grad=True), leaf(scene.shs),
+               E, leaf(scene.segments), leaf(scene.opacities), leaf(scene.scales), leaf(scene.rotations), E]
+        color, radii, depth, alpha, segment = _RasterizeGaussians.apply(*ins, st)
+        g = torch.full_like(color, 1e-3)
+        if explicit_zeros:
+            torch.autograd.backward([color, depth, alpha, segment],
+                                    [g, torch.zeros_like(depth), torch.zeros_like(alpha), torch.zeros_like(segment)])
+        else:
+            torch.autograd.backward([color], [g])
+        return [t.grad for t in ins if isinstance(t, torch.Tensor) and t.requires_grad]
+
+    for a, b in zip(run(False), run(True)):
+        torch.testing.assert_close(a, b, rtol=0, atol=0)
