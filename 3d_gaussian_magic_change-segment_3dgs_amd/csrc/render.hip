@@ -30,6 +30,8 @@
 // mean2D / conic gradients with the Gaussian's own conic and opacity.
 #include "gsr_internal.h"
 
+#include <type_traits>
+
 // Numerics.  The blend thresholds alpha >= 1/255 and T*(1-alpha) >= 1e-4
 // (forward.cu:352-359) make n_contrib and every contribution knife-edge
 // sensitive to exp(), and the reference's backward recovers T from
@@ -99,6 +101,10 @@ extern "C" __attribute__((visibility("default"))) int gsr_stats_read(unsigned lo
 
 namespace gsr {
 namespace {
+
+// Wave-wide "any": a ballot compared in SALU (HIP's __any materialises the
+// predicate in a VGPR and compares it again on the VALU).
+__device__ __forceinline__ bool wave_any(bool p) { return __builtin_amdgcn_ballot_w64(p) != 0; }
 
 constexpr float ALPHA_MIN = 1.0f / 255.0f;  // forward.cu:352
 constexpr float T_MIN = 0.0001f;            // forward.cu:355
@@ -203,7 +209,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     if (n > 0) cur = fetch_batch(rec, g_next);
     if (n > 0) g_next = plist[min(64 + lane, nlast)];
     for (int base = 0; base < n; base += 64) {
-        if (!__any((T[0] > 0.f) | (T[1] > 0.f) | (T[2] > 0.f) | (T[3] > 0.f))) break;
+        if (!wave_any((T[0] > 0.f) | (T[1] > 0.f) | (T[2] > 0.f) | (T[3] > 0.f))) break;
         const int cnt = min(64, n - base);
         STAT(5, 1);
         const Batch nxt = fetch_batch(rec, g_next);
@@ -235,7 +241,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
                 near[k] = (power[k] >= pm) & (T[k] > 0.f);
             }
             STAT(0, 1);
-            if (!__any(near[0] | near[1] | near[2] | near[3])) {
+            if (!wave_any(near[0] | near[1] | near[2] | near[3])) {
                 STAT(1, 1);
                 continue;
             }
@@ -248,7 +254,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
             // can pass; the exact reference tests below decide per pixel.
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                if (!__any(near[k])) continue;
+                if (!wave_any(near[k])) continue;
                 STAT(8, 1);
                 const float alpha = fminf(0.99f, op * GSR_EXP(power[k]));
                 const bool o = (power[k] <= 0.0f) & (alpha >= ALPHA_MIN);
@@ -406,7 +412,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) maxlast = max(maxlast, (uint32_t)__shfl_xor((int)maxlast, o, 64));
-    const bool use_bg = __any(bgdot[0] != 0.f || bgdot[1] != 0.f || bgdot[2] != 0.f || bgdot[3] != 0.f);
+    const bool use_bg = wave_any(bgdot[0] != 0.f || bgdot[1] != 0.f || bgdot[2] != 0.f || bgdot[3] != 0.f);
 
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
@@ -435,112 +441,121 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
         g_next = plist[max(top0 - 65 - lane, 0)];
         u_next = slist[max(top0 - 65 - lane, 0)];
     }
-    for (int top = top0; top > 0; top -= 64) {
-        const int cnt = min(64, top);
-        STAT(5, 1);
-        const Batch nxt = fetch_batch(rec, g_next);
-        const uint32_t u_nxt = u_next;
-        g_next = plist[max(top - 129 - lane, 0)];
-        u_next = slist[max(top - 129 - lane, 0)];
-        const float4 ra = cur.a, rb = cur.b, rc = cur.c;
-        const uint32_t uslot = u_cur;
-        cur = nxt;
-        u_cur = u_nxt;
-        const float pmin = power_floor(rb.y);
-        const bool hit = lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1);
-        uint64_t todo = __ballot(hit);
-        STAT(2, cnt - __popcll(todo));
-        __syncthreads();  // previous batch's reads are done
-        srec[lane][0] = ra;                                                   // x, y, conic a, b
-        srec[lane][1] = make_float4(rb.x, pmin, rb.y, rb.w);                  // conic c, power floor, opacity, seg0
-        srec[lane][2] = rc;                                                   // r, g, b, seg1
-        srec[lane][3] = make_float4(rb.z, __uint_as_float(uslot), 0.f, 0.f);  // depth, record slot
-        __syncthreads();
-        while (todo) {
-            const int j = (int)__builtin_ctzll(todo);
-            todo &= todo - 1;
-            const uint32_t p = (uint32_t)(top - 1 - j);
-            const float4 q0 = srec[j][0], q1 = srec[j][1];
-            const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
-            float power[4], dys[4];
-            bool near[4];
-            const float dx = gx_ - pfx;
-            const float adxdx = ca * dx * dx, bdx = cb * dx;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float dy = gy_ - pfy[k];
-                dys[k] = dy;
-                power[k] = -0.5f * (adxdx + cc * dy * dy) - bdx * dy;
-                near[k] = (p < lastc[k]) & (power[k] >= pm);
+    // The background term of dL_dalpha (backward.cu:597) is only live when bg . dL_dpix
+    // is non-zero somewhere in the tile: the loop is specialised on it.
+    auto replay = [&](auto use_bg_c) {
+        constexpr bool UB = decltype(use_bg_c)::value;
+        for (int top = top0; top > 0; top -= 64) {
+            const int cnt = min(64, top);
+            STAT(5, 1);
+            const Batch nxt = fetch_batch(rec, g_next);
+            const uint32_t u_nxt = u_next;
+            g_next = plist[max(top - 129 - lane, 0)];
+            u_next = slist[max(top - 129 - lane, 0)];
+            const float4 ra = cur.a, rb = cur.b, rc = cur.c;
+            const uint32_t uslot = u_cur;
+            cur = nxt;
+            u_cur = u_nxt;
+            const float pmin = power_floor(rb.y);
+            const bool hit = lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1);
+            uint64_t todo = __ballot(hit);
+            STAT(2, cnt - __popcll(todo));
+            __syncthreads();  // previous batch's reads are done
+            srec[lane][0] = ra;                                                   // x, y, conic a, b
+            srec[lane][1] = make_float4(rb.x, pmin, rb.y, rb.w);                  // conic c, power floor, opacity, seg0
+            srec[lane][2] = rc;                                                   // r, g, b, seg1
+            srec[lane][3] = make_float4(rb.z, __uint_as_float(uslot), 0.f, 0.f);  // depth, record slot
+            __syncthreads();
+            while (todo) {
+                const int j = (int)__builtin_ctzll(todo);
+                todo &= todo - 1;
+                const uint32_t p = (uint32_t)(top - 1 - j);
+                const float4 q0 = srec[j][0], q1 = srec[j][1];
+                const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
+                float power[4], dys[4];
+                bool near[4];
+                const float dx = gx_ - pfx;
+                const float adxdx = ca * dx * dx, bdx = cb * dx;
+    #pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float dy = gy_ - pfy[k];
+                    dys[k] = dy;
+                    power[k] = -0.5f * (adxdx + cc * dy * dy) - bdx * dy;
+                    near[k] = (p < lastc[k]) & (power[k] >= pm);
+                }
+                STAT(0, 1);
+                if (!wave_any(near[0] | near[1] | near[2] | near[3])) {
+                    STAT(1, 1);
+                    continue;
+                }
+                STAT(3, 1);
+                const float4 q2 = srec[j][2], q3 = srec[j][3];
+                const float op = q1.z, dep = q3.x, s0 = q1.w;
+                const float c0 = q2.x, c1 = q2.y, c2 = q2.z, s1 = q2.w;
+                const uint32_t u = __float_as_uint(q3.y);
+                float* dst = contrib + (size_t)u * 12;
+                float acc[12];
+    #pragma unroll
+                for (int i = 0; i < 12; ++i) acc[i] = -0.0f;  // -0 + x == x: the first add folds away
+                // Strip k (rows 4k..4k+3) is replayed only if one of its pixels can pass.
+    #pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    if (!wave_any(near[k])) continue;
+                    STAT(8, 1);
+                    const float G = GSR_EXP(power[k]);
+                    const float a = fminf(0.99f, op * G);
+                    const bool o = (p < lastc[k]) & (power[k] <= 0.0f) & (a >= ALPHA_MIN);
+                    STAT(4, POPC(o));
+                    const float one_m = 1.f - a;
+                    const float Tn = fdiv(T[k], one_m);
+                    const float dch = a * Tn;
+                    float cdot = c0 * dp0[k];
+                    cdot = __builtin_fmaf(c1, dp1[k], cdot);
+                    cdot = __builtin_fmaf(c2, dp2[k], cdot);
+                    cdot = __builtin_fmaf(s0, ds0[k], cdot);
+                    cdot = __builtin_fmaf(s1, ds1[k], cdot);
+                    cdot = __builtin_fmaf(dep, dd[k], cdot);
+                    cdot += da[k];
+                    float dopa = cdot - Dk[k];
+                    dopa *= Tn;
+                    if (UB) dopa += (-Tfin[k] * __builtin_amdgcn_rcpf(one_m)) * bgdot[k];
+                    const float dopa_m = o ? dopa : 0.f;
+                    const float dch_m = o ? dch : 0.f;
+                    acc[0] = __builtin_fmaf(dch_m, dp0[k], acc[0]);
+                    acc[1] = __builtin_fmaf(dch_m, dp1[k], acc[1]);
+                    acc[2] = __builtin_fmaf(dch_m, dp2[k], acc[2]);
+                    acc[3] = __builtin_fmaf(dch_m, ds0[k], acc[3]);
+                    acc[4] = __builtin_fmaf(dch_m, ds1[k], acc[4]);
+                    acc[5] = __builtin_fmaf(dch_m, dd[k], acc[5]);
+                    // q = G * dL_dalpha: the opacity gradient term (backward.cu:636); the
+                    // mean2D / conic terms (backward.cu:612-631) are op * q times a
+                    // polynomial in (dx, dy) with per-Gaussian coefficients, so only the
+                    // moments of q are summed here (see the record layout above).
+                    const float qg = G * dopa_m;
+                    const float qdy = qg * dys[k];
+                    acc[6] += qg;
+                    acc[8] += qdy;
+                    acc[11] = __builtin_fmaf(qdy, dys[k], acc[11]);
+                    // fold this contributor into the accumulators seen by the next one (front side)
+                    Dk[k] = o ? __builtin_fmaf(a, cdot, one_m * Dk[k]) : Dk[k];
+                    T[k] = o ? Tn : T[k];
+                }
+                acc[7] = dx * acc[6];   // sum q dx   (dx is shared by the lane's 4 pixels)
+                acc[9] = dx * acc[7];   // sum q dx^2
+                acc[10] = dx * acc[8];  // sum q dx dy
+                int vidx;
+                bool valid;
+                const float r = wave_reduce12(acc, lane, vidx, valid);
+                if (valid) dst[vidx] = r;
+                // Bit u marks slot u as written (order-independent OR: deterministic).
+                if (lane == 0) atomicOr(&written[u >> 5], 1u << (u & 31));
             }
-            STAT(0, 1);
-            if (!__any(near[0] | near[1] | near[2] | near[3])) {
-                STAT(1, 1);
-                continue;
-            }
-            STAT(3, 1);
-            const float4 q2 = srec[j][2], q3 = srec[j][3];
-            const float op = q1.z, dep = q3.x, s0 = q1.w;
-            const float c0 = q2.x, c1 = q2.y, c2 = q2.z, s1 = q2.w;
-            const uint32_t u = __float_as_uint(q3.y);
-            float* dst = contrib + (size_t)u * 12;
-            float acc[12];
-#pragma unroll
-            for (int i = 0; i < 12; ++i) acc[i] = 0.f;
-            // Strip k (rows 4k..4k+3) is replayed only if one of its pixels can pass.
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (!__any(near[k])) continue;
-                STAT(8, 1);
-                const float G = GSR_EXP(power[k]);
-                const float a = fminf(0.99f, op * G);
-                const bool o = (p < lastc[k]) & (power[k] <= 0.0f) & (a >= ALPHA_MIN);
-                STAT(4, POPC(o));
-                const float one_m = 1.f - a;
-                const float Tn = fdiv(T[k], one_m);
-                const float dch = a * Tn;
-                float cdot = c0 * dp0[k];
-                cdot = __builtin_fmaf(c1, dp1[k], cdot);
-                cdot = __builtin_fmaf(c2, dp2[k], cdot);
-                cdot = __builtin_fmaf(s0, ds0[k], cdot);
-                cdot = __builtin_fmaf(s1, ds1[k], cdot);
-                cdot = __builtin_fmaf(dep, dd[k], cdot);
-                cdot += da[k];
-                float dopa = cdot - Dk[k];
-                dopa *= Tn;
-                if (use_bg) dopa += (-Tfin[k] * __builtin_amdgcn_rcpf(one_m)) * bgdot[k];
-                const float dopa_m = o ? dopa : 0.f;
-                const float dch_m = o ? dch : 0.f;
-                acc[0] = __builtin_fmaf(dch_m, dp0[k], acc[0]);
-                acc[1] = __builtin_fmaf(dch_m, dp1[k], acc[1]);
-                acc[2] = __builtin_fmaf(dch_m, dp2[k], acc[2]);
-                acc[3] = __builtin_fmaf(dch_m, ds0[k], acc[3]);
-                acc[4] = __builtin_fmaf(dch_m, ds1[k], acc[4]);
-                acc[5] = __builtin_fmaf(dch_m, dd[k], acc[5]);
-                // q = G * dL_dalpha: the opacity gradient term (backward.cu:636); the
-                // mean2D / conic terms (backward.cu:612-631) are op * q times a
-                // polynomial in (dx, dy) with per-Gaussian coefficients, so only the
-                // moments of q are summed here (see the record layout above).
-                const float qg = G * dopa_m;
-                const float qdy = qg * dys[k];
-                acc[6] += qg;
-                acc[8] += qdy;
-                acc[11] = __builtin_fmaf(qdy, dys[k], acc[11]);
-                // fold this contributor into the accumulators seen by the next one (front side)
-                Dk[k] = o ? __builtin_fmaf(a, cdot, one_m * Dk[k]) : Dk[k];
-                T[k] = o ? Tn : T[k];
-            }
-            acc[7] = dx * acc[6];   // sum q dx   (dx is shared by the lane's 4 pixels)
-            acc[9] = dx * acc[7];   // sum q dx^2
-            acc[10] = dx * acc[8];  // sum q dx dy
-            int vidx;
-            bool valid;
-            const float r = wave_reduce12(acc, lane, vidx, valid);
-            if (valid) dst[vidx] = r;
-            // Bit u marks slot u as written (order-independent OR: deterministic).
-            if (lane == 0) atomicOr(&written[u >> 5], 1u << (u & 31));
         }
-    }
+    };
+    if (use_bg)
+        replay(std::true_type{});
+    else
+        replay(std::false_type{});
     STAT_FLUSH(16)
 }
 
