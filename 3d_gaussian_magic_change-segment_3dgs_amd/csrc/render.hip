@@ -231,17 +231,17 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
             const float4 q0 = srec[j][0], q1 = srec[j][1];
             const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
             float power[4];
-            bool near[4];
+            uint64_t near[4];  // per strip: lanes whose pixel is live and within reach
             const float dx = gx_ - pfx;
             const float adxdx = ca * dx * dx, bdx = cb * dx;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float dy = gy_ - pfy[k];
                 power[k] = -0.5f * (adxdx + cc * dy * dy) - bdx * dy;
-                near[k] = (power[k] >= pm) & (T[k] > 0.f);
+                near[k] = __builtin_amdgcn_ballot_w64(power[k] >= pm) & __builtin_amdgcn_ballot_w64(T[k] > 0.f);
             }
             STAT(0, 1);
-            if (!wave_any(near[0] | near[1] | near[2] | near[3])) {
+            if (!(near[0] | near[1] | near[2] | near[3])) {
                 STAT(1, 1);
                 continue;
             }
@@ -254,7 +254,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
             // can pass; the exact reference tests below decide per pixel.
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                if (!wave_any(near[k])) continue;
+                if (!near[k]) continue;
                 STAT(8, 1);
                 const float alpha = fminf(0.99f, op * GSR_EXP(power[k]));
                 const bool o = (power[k] <= 0.0f) & (alpha >= ALPHA_MIN);
@@ -473,7 +473,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                 const float4 q0 = srec[j][0], q1 = srec[j][1];
                 const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
                 float power[4], dys[4];
-                bool near[4];
+                uint64_t near[4];  // per strip: lanes whose pixel replays p and is within reach
                 const float dx = gx_ - pfx;
                 const float adxdx = ca * dx * dx, bdx = cb * dx;
     #pragma unroll
@@ -481,10 +481,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                     const float dy = gy_ - pfy[k];
                     dys[k] = dy;
                     power[k] = -0.5f * (adxdx + cc * dy * dy) - bdx * dy;
-                    near[k] = (p < lastc[k]) & (power[k] >= pm);
+                    near[k] = __builtin_amdgcn_ballot_w64(p < lastc[k]) & __builtin_amdgcn_ballot_w64(power[k] >= pm);
                 }
                 STAT(0, 1);
-                if (!wave_any(near[0] | near[1] | near[2] | near[3])) {
+                if (!(near[0] | near[1] | near[2] | near[3])) {
                     STAT(1, 1);
                     continue;
                 }
@@ -500,7 +500,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                 // Strip k (rows 4k..4k+3) is replayed only if one of its pixels can pass.
     #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    if (!wave_any(near[k])) continue;
+                    if (!near[k]) continue;
                     STAT(8, 1);
                     const float G = GSR_EXP(power[k]);
                     const float a = fminf(0.99f, op * G);
