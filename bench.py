@@ -108,12 +108,19 @@ def main():
     if args.gpus != world:
         if world == 1 and args.gpus > 1:
             sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    # one process per GPU; on a box with fewer GPUs than ranks (rehearsal runs with
+    # GSR_DIST_BACKEND=gloo) ranks share devices round-robin
+    dev_index = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=device)
+        backend = os.environ.get("GSR_DIST_BACKEND", "nccl")  # nccl == RCCL over xGMI on ROCm
+        if backend == "nccl":
+            dist.init_process_group(backend, device_id=device)
+        else:
+            dist.init_process_group(backend)
 
     from gsr_tools.scene import config_scene_and_camera
     from gsr_tools import dp
