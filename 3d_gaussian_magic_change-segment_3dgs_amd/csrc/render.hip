@@ -73,6 +73,10 @@ __device__ __forceinline__ float gsr_expf(float x) {
 #define GSR_EXP(x) gsr_expf(x)
 #endif
 
+// Two pixels' powers at once: v_pk_add_f32 / v_pk_mul_f32 issue both elements for the
+// price of one instruction, element by element in IEEE fp32 (same bits as scalar).
+typedef float f2 __attribute__((ext_vector_type(2)));
+
 #ifdef GSR_STATS
 // Instrumented build (tools/render_stats.py): wave-uniform loop counters, 16 per
 // kernel (fwd at 0, bwd at 16): 0 visited, 1 near-skip, 2 prefiltered out, 3 full,
@@ -235,11 +239,15 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
             const float dx = gx_ - pfx;
             const float adxdx = ca * dx * dx, bdx = cb * dx;
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float dy = gy_ - pfy[k];
-                power[k] = -0.5f * (adxdx + cc * dy * dy) - bdx * dy;
-                near[k] = __builtin_amdgcn_ballot_w64(power[k] >= pm) & __builtin_amdgcn_ballot_w64(T[k] > 0.f);
+            for (int h = 0; h < 2; ++h) {  // strips (2h, 2h+1) as one packed pair
+                const f2 dy = (f2)gy_ - (f2){pfy[2 * h], pfy[2 * h + 1]};
+                const f2 pw = (f2)(-0.5f) * ((f2)adxdx + (f2)cc * dy * dy) - (f2)bdx * dy;
+                power[2 * h] = pw.x;
+                power[2 * h + 1] = pw.y;
             }
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                near[k] = __builtin_amdgcn_ballot_w64(power[k] >= pm) & __builtin_amdgcn_ballot_w64(T[k] > 0.f);
             STAT(0, 1);
             if (!(near[0] | near[1] | near[2] | near[3])) {
                 STAT(1, 1);
