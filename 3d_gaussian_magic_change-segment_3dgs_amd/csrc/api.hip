@@ -119,6 +119,15 @@ const char* gsr_last_error(void) { return g_last_error.c_str(); }
 
 const char* gsr_version(void) { return "gsr 0.1 (gfx950)"; }
 
+int gsr_set_option(const char* name, long long value) {
+    if (!name) return fail("[gsr] option name is NULL");
+    if (std::string(name) == "sort_lookback_max") {
+        gsr::set_sort_lookback_max(value < 0 ? 0 : (size_t)value);
+        return 0;
+    }
+    return fail(std::string("[gsr] unknown option ") + name);
+}
+
 size_t gsr_geom_bytes(int P) { return gsr::geom_layout(P > 0 ? (size_t)P : 0).bytes; }
 size_t gsr_binning_bytes(int num_rendered) { return gsr::bin_layout(num_rendered > 0 ? (size_t)num_rendered : 0).bytes; }
 size_t gsr_img_bytes(int W, int H) { return gsr::img_layout(W, H).bytes; }

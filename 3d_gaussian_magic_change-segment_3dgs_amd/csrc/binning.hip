@@ -480,7 +480,9 @@ void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_id
 
 int depth_sort_passes() { return 4; }
 int sort_lb_items() { return GSR_LB_ITEMS; }
-bool sort_uses_lookback(size_t n) { return n <= GSR_SORT_LB_MAX; }
+static size_t g_sort_lb_max = GSR_SORT_LB_MAX;  // gsr_set_option("sort_lookback_max", n)
+void set_sort_lookback_max(size_t n) { g_sort_lb_max = n; }
+bool sort_uses_lookback(size_t n) { return n <= g_sort_lb_max; }
 
 template <int ITEMS, bool LB>
 static void launch_scatter(size_t n, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
@@ -501,7 +503,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
     const int per_pass = (key_bits + passes - 1) / passes;  // balanced: 13 bits -> 7 + 6
     const SortWs W = sort_ws(n, ws);
-    const bool lb = n <= GSR_SORT_LB_MAX;
+    const bool lb = sort_uses_lookback(n);
     if (lb) {
         const size_t nt = sort_tiles(n, GSR_LB_ITEMS);
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, GSR_LB_ITEMS), st);

@@ -171,6 +171,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL =
 int depth_sort_passes();
 int sort_lb_items();
 bool sort_uses_lookback(size_t n);
+void set_sort_lookback_max(size_t n);
 void launch_tile_order(const uint2* ranges, int T, uint32_t* order, hipStream_t st);
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
                                   void* ws, bool ws_zeroed, hipStream_t st);

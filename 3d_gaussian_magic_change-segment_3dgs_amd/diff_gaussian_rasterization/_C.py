@@ -70,6 +70,8 @@ _lib.gsr_version.restype = ctypes.c_char_p
 _lib.gsr_debug_copy.restype = ctypes.c_longlong
 _lib.gsr_debug_copy.argtypes = [ctypes.c_char_p, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]
 
+_lib.gsr_set_option.restype = _i
+_lib.gsr_set_option.argtypes = [ctypes.c_char_p, ctypes.c_longlong]
 _lib.gsr_num_stages.restype = _i
 _lib.gsr_stage_name.restype = ctypes.c_char_p
 _lib.gsr_stage_name.argtypes = [_i]
@@ -80,7 +82,7 @@ _lib.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POIN
 EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_img_bytes", "gsr_backward_scratch_bytes",
                     "gsr_forward_geometry", "gsr_forward_render", "gsr_backward", "gsr_mark_visible",
                     "gsr_debug_copy", "gsr_num_stages", "gsr_stage_name", "gsr_timing_enable", "gsr_timing_collect",
-                    "gsr_last_error", "gsr_version")
+                    "gsr_last_error", "gsr_version", "gsr_set_option")
 
 _DEBUG_FIELDS = {  # name -> (dtype, elements per unit, unit: P | I | T)
     "tiles_touched": (torch.int32, 1, "P"), "rec": (torch.float32, 16, "P"), "clamped": (torch.uint8, 1, "P"),
@@ -220,6 +222,11 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
                                        img.data_ptr(), num_rendered, color.data_ptr(), depth.data_ptr(),
                                        alpha.data_ptr(), segment.data_ptr(), stream))
     return num_rendered, color, depth, segment, alpha, radii, geom, binning, img
+
+
+def set_option(name, value):
+    """Process-wide tuning / test hook (include/gsr.h: gsr_set_option)."""
+    _check(_lib.gsr_set_option(name.encode(), int(value)))
 
 
 def grad_arena_layout(P, M):

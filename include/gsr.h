@@ -170,6 +170,11 @@ GSR_API const char* gsr_last_error(void);
 
 /* Library version string (build identification). */
 GSR_API const char* gsr_version(void);
+/* ---- tuning / test hook (process-wide, not thread-safe against concurrent calls):
+ * "sort_lookback_max": radix sorts of at most this many keys use the single-launch
+ * look-back passes, larger ones the histogram-table passes (default 4194304).
+ * Results are identical either way.  Returns 0, or non-zero for an unknown name. */
+GSR_API int gsr_set_option(const char* name, long long value);
 
 #ifdef __cplusplus
 }

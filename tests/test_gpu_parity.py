@@ -193,3 +193,16 @@ def test_zero_gaussians(gpu_available):
                                  rotations=torch.zeros(0, 4, device="cuda"))
     color, radii, depth, alpha, segment = out
     assert color.shape == (3, 32, 48) and float(color.abs().sum()) == 0.0 and radii.numel() == 0
+
+
+def test_table_mode_sorts(gpu_available, oracle_mod):
+    """Sorts above the look-back threshold (P or I > 4M at the defaults: the 3M / 6M
+    Gaussian configs) take the histogram-table passes; force them on a small scene."""
+    from diff_gaussian_rasterization import _C
+    scene = synthetic_scene(30000, sh_degree=3, seed=24)
+    cam = orbit_camera(6, 400, 300, 330.0)
+    try:
+        _C.set_option("sort_lookback_max", 0)
+        compare(oracle_mod, scene, cam)
+    finally:
+        _C.set_option("sort_lookback_max", 4 << 20)

@@ -30,3 +30,9 @@ if len(starts) > 1:
 items = sorted(gap.items(), key=lambda kv: -sum(kv[1]) / len(kv[1]))
 for (n0, n1), v in items[:25]:
     print(f"  {sum(v) / len(v) / 1e3:8.1f} us  {n0} -> {n1}")
+
+# per-kernel durations in the last step (launch order)
+a, b = steps[-1]
+print("last step kernels:")
+for s0, e0, n0 in ks[a:b]:
+    print(f"  {(e0 - s0) / 1e3:8.1f} us  {n0}")
