@@ -155,6 +155,8 @@ CONFIGS = {
     "mt": dict(P=1_000_000, sh_degree=3, width=1920, height=1080, focal=1200.0, extent=1.5),
     # C3: garden-like 3M, SH3, 1080p
     "c3": dict(P=3_000_000, sh_degree=3, width=1920, height=1080, focal=1200.0, extent=1.5),
+    # C5: 6M = two 3M scenes merged (visualizer.py:196-226), SH3, 1080p
+    "c5": dict(P=3_000_000, sh_degree=3, width=1920, height=1080, focal=1200.0, extent=1.5, merge=2),
 }
 
 
@@ -166,6 +168,11 @@ def config_scene_and_camera(name, view_index=0, n_views=8, P=None, seed=0):
     if "log_scale" in c:
         kw["log_scale"] = c["log_scale"]
     scene = synthetic_scene(c["P"], sh_degree=c["sh_degree"], extent=c["extent"], seed=seed, **kw)
+    for m in range(1, c.get("merge", 1)):  # concatenate independently seeded scenes
+        other = synthetic_scene(c["P"], sh_degree=c["sh_degree"], extent=c["extent"], seed=seed + m, **kw)
+        scene = Scene(*(torch.cat([getattr(scene, f), getattr(other, f)], 0).contiguous()
+                        for f in ("means3D", "shs", "opacities", "scales", "rotations", "segments")),
+                      scene.sh_degree)
     W, H = c["width"], c["height"]
     if "focal" in c:
         focal = c["focal"]
