@@ -88,6 +88,30 @@ __device__ __forceinline__ int lb_tile_index(uint32_t* counter) {
     return s_tile;
 }
 
+// Exclusive scan over a block of WAVES wave64s.  wsum: __shared__ uint32_t[WAVES].
+template <int WAVES>
+__device__ __forceinline__ uint32_t block_exclusive_scan_w(uint32_t v, uint32_t* wsum, uint32_t* total) {
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t y = __shfl_up(x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) wsum[wid] = x;
+    __syncthreads();
+    uint32_t pre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WAVES; ++w) {
+        const uint32_t s = wsum[w];
+        if (w < wid) pre += s;
+        tot += s;
+    }
+    __syncthreads();
+    *total = tot;
+    return pre + x - v;
+}
+
 // ---------------------------------------------------------------- scan ----
 // out[i] = sum_{j<=i (INCLUSIVE) / j<i} value(j), value(j) = gather ? src[gather[j]] : src[j], in one
 // pass: each tile of 4096 values is staged through LDS (coalesced loads/stores),
@@ -188,17 +212,18 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __r
 // Per-tile digit histogram -> hist[digit * ntiles + tile] (table-driven passes).
 // Equal digits of a wave round are counted by their first lane (ballot multisplit),
 // so skewed digit distributions do not serialise on one LDS address.
-template <int ITEMS>
-__global__ void __launch_bounds__(SORT_THREADS) k_radix_upsweep(const uint32_t* __restrict__ keys, size_t n,
-                                                                int shift, int bits, uint32_t* __restrict__ hist,
-                                                                void* scan_ws, size_t scan_ws16) {
+template <int ITEMS, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) k_radix_upsweep(const uint32_t* __restrict__ keys, size_t n,
+                                                              int shift, int bits, uint32_t* __restrict__ hist,
+                                                              void* scan_ws, size_t scan_ws16) {
+    constexpr int NT = 64 * WAVES;
     __shared__ uint32_t cnt[RADIX];
-    zero16(scan_ws, scan_ws16, (size_t)blockIdx.x * SORT_THREADS + threadIdx.x, (size_t)gridDim.x * SORT_THREADS);
+    zero16(scan_ws, scan_ws16, (size_t)blockIdx.x * NT + threadIdx.x, (size_t)gridDim.x * NT);
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t ndig = 1u << bits, mask = ndig - 1u;
-    cnt[tid] = 0;
+    for (int i = tid; i < RADIX; i += NT) cnt[i] = 0;
     __syncthreads();
-    const size_t wbase = (size_t)blockIdx.x * (SORT_THREADS * ITEMS) + (size_t)wid * (64 * ITEMS);
+    const size_t wbase = (size_t)blockIdx.x * (NT * ITEMS) + (size_t)wid * (64 * ITEMS);
     uint32_t key[ITEMS];
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
@@ -218,7 +243,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_upsweep(const uint32_t* 
         if (valid && __popcll(peers & lanemask_lt()) == 0) atomicAdd(&cnt[digit], (uint32_t)__popcll(peers));
     }
     __syncthreads();
-    if ((uint32_t)tid < ndig) hist[(size_t)tid * gridDim.x + blockIdx.x] = cnt[tid];
+    for (int d = tid; d < (int)ndig; d += NT) hist[(size_t)d * gridDim.x + blockIdx.x] = cnt[d];
 }
 
 // Stable scatter, staged through LDS, one launch per pass.  Wave w of the tile ranks the elements
@@ -238,23 +263,23 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_upsweep(const uint32_t* 
 // LB = false: they come from a scanned per-tile histogram table (hist[d * ntiles + t],
 // k_radix_upsweep + k_scan<false>): more launches, but no look-back latency chain,
 // which costs a cross-XCD round trip per hop on MI355X.
-template <int ITEMS, bool LB>
-__global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
+template <int ITEMS, int WAVES, bool LB>
+__global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, size_t n, int shift, int bits, const uint32_t* __restrict__ hist,
     uint64_t* status, uint32_t* counter, const uint32_t* __restrict__ vals2_in, uint32_t* __restrict__ vals2_out) {
-    constexpr int TILE = SORT_THREADS * ITEMS;
+    constexpr int NT = 64 * WAVES, TILE = NT * ITEMS;
     __shared__ uint32_t s_key[TILE], s_val[TILE], s_val2[TILE];
-    __shared__ uint32_t wcnt[4][RADIX];
+    __shared__ uint32_t wcnt[WAVES][RADIX];
     __shared__ uint32_t dbase[RADIX], gbase[RADIX];
-    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t wsum[WAVES];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t ndig = 1u << bits, mask = ndig - 1u;
     const int t = LB ? lb_tile_index(counter) : (int)blockIdx.x;
 #pragma unroll
     for (int i = 0; i < RADIX / 64; ++i) wcnt[wid][lane + 64 * i] = 0;
     const size_t bbase = (size_t)t * TILE;
-    const size_t wbase = bbase + (size_t)wid * (TILE / 4);
+    const size_t wbase = bbase + (size_t)wid * (64 * ITEMS);
     const uint64_t lt = lanemask_lt();
     uint32_t key[ITEMS], val[ITEMS], val2[ITEMS], rk[ITEMS];
 #pragma unroll
@@ -283,23 +308,23 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
     }
     __syncthreads();
     // digit-major block offsets: dbase[d] = elements of digits < d; wave offsets inside d
-    uint32_t c[4], tot = 0;
+    uint32_t tot = 0;
+    if ((uint32_t)tid < ndig)
 #pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        c[w] = (uint32_t)tid < ndig ? wcnt[w][tid] : 0u;
-        tot += c[w];
-    }
+        for (int w = 0; w < WAVES; ++w) tot += wcnt[w][tid];
     uint32_t total;
-    const uint32_t db = block_exclusive_scan(tot, wsum, &total);
+    const uint32_t db = block_exclusive_scan_w<WAVES>(tot, wsum, &total);
     // global start of each digit (exclusive scan of the pass histogram)
-    const uint32_t gstart = LB ? block_exclusive_scan((uint32_t)tid < ndig ? hist[tid] : 0u, wsum, &total) : 0u;
+    const uint32_t gstart =
+        LB ? block_exclusive_scan_w<WAVES>((uint32_t)tid < ndig ? hist[tid] : 0u, wsum, &total) : 0u;
     if ((uint32_t)tid < ndig) {
         dbase[tid] = db;
         uint32_t o = db;
 #pragma unroll
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < WAVES; ++w) {
+            const uint32_t cw = wcnt[w][tid];
             wcnt[w][tid] = o;
-            o += c[w];
+            o += cw;
         }
         if (LB) {
             // this tile's offset inside digit tid: decoupled look-back over earlier tiles
@@ -330,7 +355,7 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_scatter(
     }
     __syncthreads();
     const int nvalid = (int)min((size_t)TILE, n - bbase);
-    for (int p = tid; p < nvalid; p += SORT_THREADS) {
+    for (int p = tid; p < nvalid; p += NT) {
         const uint32_t k = s_key[p];
         const uint32_t d = (k >> shift) & mask;
         const size_t g = (size_t)gbase[d] + (uint32_t)p - dbase[d];
@@ -472,24 +497,33 @@ void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_id
 #define GSR_SORT_LB_MAX (4u << 20)
 #endif
 #ifndef GSR_LB_ITEMS
-#define GSR_LB_ITEMS 16
+#define GSR_LB_ITEMS 4
+#endif
+#ifndef GSR_LB_WAVES
+#define GSR_LB_WAVES 16
+#endif
+#ifndef GSR_TB_WAVES
+#define GSR_TB_WAVES 16
 #endif
 #ifndef GSR_TB_ITEMS
-#define GSR_TB_ITEMS 8
+#define GSR_TB_ITEMS 4
 #endif
 
 int depth_sort_passes() { return 4; }
-int sort_lb_items() { return GSR_LB_ITEMS; }
+int sort_lb_items() { return GSR_LB_ITEMS * GSR_LB_WAVES / 4; }  // in units of 256-element rows
 static size_t g_sort_lb_max = GSR_SORT_LB_MAX;  // gsr_set_option("sort_lookback_max", n)
 void set_sort_lookback_max(size_t n) { g_sort_lb_max = n; }
 bool sort_uses_lookback(size_t n) { return n <= g_sort_lb_max; }
 
-template <int ITEMS, bool LB>
+// A tile is 64 * WAVES * ITEMS elements; sort_tiles(n, WAVES * ITEMS / 4) counts them.
+template <int ITEMS, int WAVES, bool LB>
 static void launch_scatter(size_t n, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
                            int shift, int bits, const uint32_t* hist, uint64_t* status, uint32_t* counter,
                            const uint32_t* v2in, uint32_t* v2out, hipStream_t st) {
-    hipLaunchKernelGGL((k_radix_scatter<ITEMS, LB>), dim3(sort_tiles(n, ITEMS)), dim3(SORT_THREADS), 0, st, kin,
-                       vin, kout, vout, n, shift, bits, hist, status, counter, v2in, v2out);
+    static_assert(WAVES * ITEMS % 4 == 0, "tile must be a multiple of 256 elements");
+    hipLaunchKernelGGL((k_radix_scatter<ITEMS, WAVES, LB>), dim3(sort_tiles(n, WAVES * ITEMS / 4)),
+                       dim3(64 * WAVES), 0, st, kin, vin, kout, vout, n, shift, bits, hist, status, counter, v2in,
+                       v2out);
 }
 
 // Stable LSD sort of (keys, vals[, vals2]) on the low key_bits bits.  Ping-pongs
@@ -505,8 +539,8 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     const SortWs W = sort_ws(n, ws);
     const bool lb = sort_uses_lookback(n);
     if (lb) {
-        const size_t nt = sort_tiles(n, GSR_LB_ITEMS);
-        if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, GSR_LB_ITEMS), st);
+        const size_t nt = sort_tiles(n, sort_lb_items());
+        if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);
         hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)min(nt, (size_t)1024)), dim3(SORT_THREADS), 0, st, keys_in,
                            n, passes, per_pass, key_bits, W.hist);
     }
@@ -522,19 +556,21 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
         uint32_t* vout = to_out ? vals_out : vals_tmp;
         uint32_t* v2out = vals2_in ? (to_out ? vals2_out : vals2_tmp) : nullptr;
         if (lb) {
-            const size_t nt = sort_tiles(n, GSR_LB_ITEMS);
-            launch_scatter<GSR_LB_ITEMS, true>(n, kin, vin, kout, vout, shift, bits, W.hist + p * RADIX,
-                                               W.status + (size_t)p * nt * RADIX, W.counter + p, v2in, v2out, st);
+            const size_t nt = sort_tiles(n, sort_lb_items());
+            launch_scatter<GSR_LB_ITEMS, GSR_LB_WAVES, true>(n, kin, vin, kout, vout, shift, bits,
+                                                             W.hist + p * RADIX, W.status + (size_t)p * nt * RADIX,
+                                                             W.counter + p, v2in, v2out, st);
         } else {
-            const size_t nt = sort_tiles(n, GSR_TB_ITEMS);
+            const size_t nt = sort_tiles(n, GSR_TB_ITEMS * GSR_TB_WAVES / 4);
             const size_t len = ((size_t)1 << bits) * nt;
             const ScanWs S = scan_ws(len, W.scan);
-            hipLaunchKernelGGL(k_radix_upsweep<GSR_TB_ITEMS>, dim3(nt), dim3(SORT_THREADS), 0, st, kin, n, shift,
+            hipLaunchKernelGGL((k_radix_upsweep<GSR_TB_ITEMS, GSR_TB_WAVES>), dim3(nt), dim3(64 * GSR_TB_WAVES), 0, st,
+                               kin, n, shift,
                                bits, W.table, S.base, cdiv(S.bytes, 16));
             hipLaunchKernelGGL(k_scan<false>, dim3(cdiv(len, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, W.table,
                                nullptr, len, W.table, S.status, S.counter);
-            launch_scatter<GSR_TB_ITEMS, false>(n, kin, vin, kout, vout, shift, bits, W.table, nullptr, nullptr,
-                                                v2in, v2out, st);
+            launch_scatter<GSR_TB_ITEMS, GSR_TB_WAVES, false>(n, kin, vin, kout, vout, shift, bits, W.table, nullptr,
+                                                              nullptr, v2in, v2out, st);
         }
         kin = kout;
         vin = vout;
