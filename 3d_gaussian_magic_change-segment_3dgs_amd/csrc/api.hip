@@ -2,6 +2,7 @@
 // Reference orchestration: DGR/cuda_rasterizer/rasterizer_impl.cu:198-458 and
 // the host bindings DGR/rasterize_points.cu:35-242.
 #include <stdio.h>
+#include <stdlib.h>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -113,6 +114,69 @@ int validate(const gsr_settings* s, const gsr_inputs* in, bool forward) {
 
 }  // namespace
 
+namespace {
+
+// num_rendered hand-off.  The scan writes the total into a host-mapped pinned word
+// (one per host thread: calls from one thread are sequential, and this call waits for
+// the value before returning); the host polls it, which returns as soon as the scan's
+// last tile is done instead of after a copy kernel and a stream synchronisation.  If
+// the stream drains without the value appearing (or pinned memory is unavailable) the
+// total is copied the ordinary way.
+constexpr uint32_t TOTAL_PENDING = 0xFFFFFFFFu;
+struct HostSlot {
+    uint32_t* host = nullptr;  // CPU view
+    uint32_t* dev = nullptr;   // GPU view of the same pinned word
+};
+HostSlot host_total_slot() {
+    thread_local HostSlot slot;
+    thread_local bool tried = false;
+    if (!tried) {
+        tried = true;
+        const char* env = getenv("GSR_HOST_TOTAL");
+        if (env && env[0] == '0') return slot;
+        void* p = nullptr;
+        void* d = nullptr;
+        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+            if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess) {
+                slot.host = (uint32_t*)p;
+                slot.dev = (uint32_t*)d;
+            } else {
+                (void)hipHostFree(p);
+            }
+        }
+    }
+    return slot;
+}
+int wait_total(uint32_t* hslot, hipStream_t st, const uint32_t* dev_last, uint32_t* total) {
+    if (hslot) {
+        for (unsigned spin = 0;; ++spin) {
+            const uint32_t v = __atomic_load_n(hslot, __ATOMIC_ACQUIRE);
+            if (v != TOTAL_PENDING) {
+                *total = v;
+                return 0;
+            }
+            if ((spin & 255u) == 255u) {
+                const hipError_t q = hipStreamQuery(st);
+                if (q == hipSuccess) {  // drained: read once more, then fall back
+                    const uint32_t w = __atomic_load_n(hslot, __ATOMIC_ACQUIRE);
+                    if (w != TOTAL_PENDING) {
+                        *total = w;
+                        return 0;
+                    }
+                    break;
+                }
+                if (q != hipErrorNotReady) return fail(std::string("[gsr] num_rendered: ") + hipGetErrorString(q));
+            }
+        }
+    }
+    hipError_t e = hipMemcpyAsync(total, dev_last, sizeof(uint32_t), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return fail(std::string("[gsr] num_rendered copy: ") + hipGetErrorString(e));
+    return 0;
+}
+
+}  // namespace
+
 extern "C" {
 
 const char* gsr_last_error(void) { return g_last_error.c_str(); }
@@ -150,6 +214,9 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
     const ImgLayout IL = img_layout(s->W, s->H);
     const GeomLayout L = geom_layout(P);
     char* g = aligned_base(geom);
+    const HostSlot hs = host_total_slot();  // NULL views if pinned host memory is unavailable
+    uint32_t* hslot = hs.host;
+    if (hslot) __atomic_store_n(hslot, TOTAL_PENDING, __ATOMIC_RELAXED);
     {
         StageScope sc(GSR_STAGE_PREPROCESS, st);
         const bool lb = sort_uses_lookback(P);
@@ -170,14 +237,11 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
     {
         StageScope sc(GSR_STAGE_SCAN, st);
         launch_scan_inclusive_gather(at<uint32_t>(g, L.tiles_touched), at<uint32_t>(g, L.order),
-                                     at<uint32_t>(g, L.offsets), P, g + L.ws_scan, /*ws_zeroed=*/true, st);
+                                     at<uint32_t>(g, L.offsets), P, g + L.ws_scan, /*ws_zeroed=*/true, st, hs.dev);
     }
     GSR_STAGE("scan");
     uint32_t total = 0;
-    hipError_t e = hipMemcpyAsync(&total, at<uint32_t>(g, L.offsets) + (P - 1), sizeof(uint32_t),
-                                  hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-    if (e != hipSuccess) return fail(std::string("[gsr] num_rendered copy: ") + hipGetErrorString(e));
+    if (int rc = wait_total(hslot, st, at<uint32_t>(g, L.offsets) + (P - 1), &total)) return rc;
     if (total > 0x7FFFFFFFu) return fail("[gsr] num_rendered overflows int32");
     *num_rendered = (int)total;
     return 0;

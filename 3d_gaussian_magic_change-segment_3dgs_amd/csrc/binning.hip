@@ -120,7 +120,7 @@ template <bool INCLUSIVE>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restrict__ src,
                                                        const uint32_t* __restrict__ gather, size_t n,
                                                        uint32_t* __restrict__ out, uint64_t* status,
-                                                       uint32_t* counter) {
+                                                       uint32_t* counter, uint32_t* host_total) {
     __shared__ uint32_t tile[SCAN_TILE + SCAN_TILE / 32];
     __shared__ uint32_t wsum[4];
     __shared__ uint32_t s_excl;
@@ -182,6 +182,10 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restric
         const int li = i * SCAN_THREADS + threadIdx.x;
         const size_t idx = base + li;
         if (idx < n) out[idx] = tile[pad(li)];
+        // the grand total, straight into host-mapped memory (system-scope store): the
+        // host polls it instead of waiting for a copy + stream synchronisation
+        if (host_total && idx == n - 1)
+            __hip_atomic_store(host_total, tile[pad(li)], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
 }
 
@@ -481,12 +485,12 @@ uint32_t higher_msb(uint32_t n) {
 }
 
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
-                                  void* ws, bool ws_zeroed, hipStream_t st) {
+                                  void* ws, bool ws_zeroed, hipStream_t st, uint32_t* host_total) {
     if (n == 0) return;
     const ScanWs W = scan_ws(n, ws);
     if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, W.bytes, st);
     hipLaunchKernelGGL(k_scan<true>, dim3(cdiv(n, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, src, gather_idx, n, out,
-                       W.status, W.counter);
+                       W.status, W.counter, host_total);
 }
 
 // Sorting modes (measured on MI355X): small sorts are launch-bound and use one
@@ -568,7 +572,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
                                kin, n, shift,
                                bits, W.table, S.base, cdiv(S.bytes, 16));
             hipLaunchKernelGGL(k_scan<false>, dim3(cdiv(len, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, W.table,
-                               nullptr, len, W.table, S.status, S.counter);
+                               nullptr, len, W.table, S.status, S.counter, nullptr);
             launch_scatter<GSR_TB_ITEMS, GSR_TB_WAVES, false>(n, kin, vin, kout, vout, shift, bits, W.table, nullptr,
                                                               nullptr, v2in, v2out, st);
         }

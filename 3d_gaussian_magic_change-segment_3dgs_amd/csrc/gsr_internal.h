@@ -174,7 +174,7 @@ bool sort_uses_lookback(size_t n);
 void set_sort_lookback_max(size_t n);
 void launch_tile_order(const uint2* ranges, int T, uint32_t* order, hipStream_t st);
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
-                                  void* ws, bool ws_zeroed, hipStream_t st);
+                                  void* ws, bool ws_zeroed, hipStream_t st, uint32_t* host_total = nullptr);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, int gx, uint32_t* tkeys, uint32_t* slot_gid, uint32_t* goff,
                       uint2* ranges, int T, hipStream_t st);

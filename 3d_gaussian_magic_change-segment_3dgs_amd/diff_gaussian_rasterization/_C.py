@@ -137,6 +137,10 @@ def _dev_f32(t, device, name, align=4):
     return t
 
 
+_BIN_GUESS = os.environ.get("GSR_BIN_GUESS", "1") != "0"
+_last_rendered = {}  # device -> num_rendered of the last forward (binning size guess)
+
+
 def _ptr(t):
     return None if t is None else t.data_ptr()
 
@@ -213,11 +217,19 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
         depth = torch.empty(1, H, W, **f32)
         alpha = torch.empty(1, H, W, **f32)
         segment = torch.empty(NUM_CLASS, H, W, **f32)
+        # The binning buffer depends on num_rendered, known only after the geometry
+        # stage; allocate a guess (the last count on this device + 15%) before it so
+        # that nothing but the render launches sits between the sync and the GPU.
+        cap = _last_rendered.get(device, 0)
+        cap = cap + cap // 7 + 4096 if cap and _BIN_GUESS else 0
+        binning = torch.empty(_lib.gsr_binning_bytes(cap), **u8) if cap else None
         nr = ctypes.c_int(0)
         _check(_lib.gsr_forward_geometry(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), radii.data_ptr(),
                                          stream, ctypes.byref(nr)))
         num_rendered = int(nr.value)
-        binning = torch.empty(_lib.gsr_binning_bytes(num_rendered), **u8)
+        _last_rendered[device] = num_rendered
+        if binning is None or num_rendered > cap:
+            binning = torch.empty(_lib.gsr_binning_bytes(num_rendered), **u8)
         _check(_lib.gsr_forward_render(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), binning.data_ptr(),
                                        img.data_ptr(), num_rendered, color.data_ptr(), depth.data_ptr(),
                                        alpha.data_ptr(), segment.data_ptr(), stream))
