@@ -177,6 +177,10 @@ int wait_total(uint32_t* hslot, hipStream_t st, const uint32_t* dev_last, uint32
 
 }  // namespace
 
+namespace gsr {
+int set_error(const std::string& msg) { return fail(msg); }
+}  // namespace gsr
+
 extern "C" {
 
 const char* gsr_last_error(void) { return g_last_error.c_str(); }

@@ -4,9 +4,14 @@
 #include <stdint.h>
 #include <stddef.h>
 
+#include <string>
+
 #include "../../include/gsr.h"
 
 namespace gsr {
+
+// Sets the thread-local gsr_last_error() message; returns 1 (api.hip).
+int set_error(const std::string& msg);
 
 constexpr int BX = GSR_BLOCK_X, BY = GSR_BLOCK_Y;
 constexpr int NCH = GSR_NUM_CHANNELS, NCLS = GSR_NUM_CLASS;

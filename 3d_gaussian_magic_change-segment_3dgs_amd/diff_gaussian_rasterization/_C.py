@@ -23,6 +23,7 @@ _lib = ctypes.CDLL(LIB_PATH)
 
 NUM_CHANNELS = 3  # config.h:15
 NUM_CLASS = 2     # config.h:16
+ARENA_ALIGN = 64  # include/gsr_train.h GSR_ARENA_ALIGN (floats)
 
 
 class _Settings(ctypes.Structure):
@@ -70,6 +71,11 @@ _lib.gsr_version.restype = ctypes.c_char_p
 _lib.gsr_debug_copy.restype = ctypes.c_longlong
 _lib.gsr_debug_copy.argtypes = [ctypes.c_char_p, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]
 
+_ll = ctypes.c_longlong
+_lib.gsr_arena_layout.restype = _ll
+_lib.gsr_arena_layout.argtypes = [_i, _i, _i, ctypes.POINTER(_ll)]
+_lib.gsr_act_layout.restype = _ll
+_lib.gsr_act_layout.argtypes = [_i, _i, ctypes.POINTER(_ll)]
 _lib.gsr_set_option.restype = _i
 _lib.gsr_set_option.argtypes = [ctypes.c_char_p, ctypes.c_longlong]
 _lib.gsr_num_stages.restype = _i
@@ -245,17 +251,22 @@ def grad_arena_layout(P, M):
     """Offsets (in floats) of the gradients inside the single arena allocated by
     rasterize_gaussians_backward.  The first `bucket` floats are the parameter
     gradients a data-parallel trainer all-reduces: [dmeans3D | dsh | dopacity |
-    dscales | drot | dsegments]; means2D/colour/cov3D grads follow."""
-    sizes = [("dmeans3D", 3), ("dsh", 3 * M), ("dopacity", 1), ("dscales", 3), ("drot", 4),
-             ("dsegments", NUM_CLASS), ("dmeans2D", 3), ("dcolors", 3), ("dcov3D", 6)]
-    off, o = {}, 0
-    for n, k in sizes:
-        off[n] = (o, k)
-        o += k * P
-        if n == "dsegments":
-            off["bucket"] = (0, o)
-    off["total"] = (0, o)
-    return off
+    dscales | drot | dsegments], laid out exactly like the
+    training arena of include/gsr_train.h (every block 64-float aligned), so the
+    bucket is also the gradient of the trainer's parameter arena; means2D /
+    colour / cov3D grads follow.  Maps name -> (offset, floats per Gaussian)."""
+    off = (ctypes.c_longlong * 7)()
+    _lib.gsr_arena_layout(P, M, NUM_CLASS, off)
+    names = [("dmeans3D", 3), ("dsh", 3 * M), ("dopacity", 1), ("dscales", 3), ("drot", 4),
+             ("dsegments", NUM_CLASS)]
+    lay = {n: (int(off[b]), k) for b, (n, k) in enumerate(names)}
+    lay["bucket"] = (0, int(off[6]))
+    o = int(off[6])
+    for n, k in (("dmeans2D", 3), ("dcolors", 3), ("dcov3D", 6)):
+        lay[n] = (o, k)
+        o += -(-k * P // ARENA_ALIGN) * ARENA_ALIGN
+    lay["total"] = (0, o)
+    return lay
 
 
 def rasterize_gaussians_backward(background, means3D, radii, colors, segments, scales, rotations, scale_modifier,

@@ -10,10 +10,11 @@ import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "gsr.h")
+TRAIN_HEADER = os.path.join(ROOT, "include", "gsr_train.h")
 
 
-def declared_symbols():
-    txt = open(HEADER).read()
+def declared_symbols(header=HEADER):
+    txt = open(header).read()
     return sorted(set(re.findall(r"GSR_API\s+[\w\s\*]*?\b(gsr_\w+)\s*\(", txt)))
 
 
@@ -31,6 +32,44 @@ def test_library_exports_every_declared_symbol():
         assert hasattr(lib, s), f"{s} declared in include/gsr.h but not exported"
     assert sorted(_C.EXPORTED_SYMBOLS) == declared_symbols()
     assert _C.version().startswith("gsr")
+
+
+def test_library_exports_every_training_symbol():
+    """include/gsr_train.h (SURVEY.md s8f kernels) is exported by the same library."""
+    from diff_gaussian_rasterization import _C
+    from gsr_train import _C as T
+    lib = ctypes.CDLL(_C.LIB_PATH)
+    syms = declared_symbols(TRAIN_HEADER)
+    assert "gsr_adam_step" in syms and "gsr_activate" in syms
+    for s in syms:
+        assert hasattr(lib, s), f"{s} declared in include/gsr_train.h but not exported"
+    assert sorted(T.EXPORTED_SYMBOLS) == syms
+
+
+def test_training_calls_validate_without_the_device():
+    from gsr_train import _C as T
+    L = T._lib
+    h = T.AdamHyper()
+    assert L.gsr_adam_step(10, 16, 2, None, None, None, None, None, ctypes.byref(h), None) != 0
+    assert b"null buffer" in L.gsr_last_error()
+    assert L.gsr_adam_step(10, 17, 2, 16, 16, 16, 16, None, ctypes.byref(h), None) != 0
+    assert b"invalid" in L.gsr_last_error()
+    assert L.gsr_adam_step(0, 16, 2, None, None, None, None, None, ctypes.byref(h), None) == 0  # empty: no-op
+    assert L.gsr_densify_stats(5, None, None, 16, None, 16, 16, None) != 0
+
+
+def test_arena_spec_views_cover_reference_shapes():
+    from gsr_train import ArenaSpec
+    s = ArenaSpec(1001, 16)
+    a = torch.arange(s.total, dtype=torch.float32)
+    assert s.group(a, "f_dc").shape == (1001, 1, 3) and s.group(a, "f_rest").shape == (1001, 15, 3)
+    assert s.group(a, "rotation").shape == (1001, 4) and s.group(a, "segment").shape == (1001, 2)
+    assert float(s.group(a, "f_dc")[1, 0, 0]) == s.off[1] + 48  # [P,M,3] row-major, coefficient 0 first
+    touched = torch.zeros(s.total, dtype=torch.int32)
+    for n in ("xyz", "features", "opacity", "scaling", "rotation", "segment"):
+        touched[s.off[("xyz", "features", "opacity", "scaling", "rotation", "segment").index(n)]:][
+            :s.width[n] * s.P] += 1
+    assert int(touched.max()) == 1  # blocks are disjoint
 
 
 def test_size_queries():
@@ -79,7 +118,19 @@ def test_python_api_rejects_cpu_tensors():
 
 
 def test_grad_arena_layout_bucket_first():
+    """The all-reduce bucket leads the gradient arena and matches the training
+    arena of include/gsr_train.h block for block (64-float aligned blocks)."""
+    import ctypes
     from diff_gaussian_rasterization import _C
-    lay = _C.grad_arena_layout(10, 16)
-    assert lay["bucket"] == (0, 10 * (3 + 48 + 1 + 3 + 4 + 2))
-    assert lay["dmeans3D"][0] == 0 and lay["dsegments"][0] + 20 == lay["bucket"][1]
+    for P, M in ((10, 16), (1, 1), (1000, 9), (4097, 16)):
+        lay = _C.grad_arena_layout(P, M)
+        off = (ctypes.c_longlong * 7)()
+        total = _C._lib.gsr_arena_layout(P, M, 2, off)
+        names = ("dmeans3D", "dsh", "dopacity", "dscales", "drot", "dsegments")
+        assert [lay[n][0] for n in names] == list(off)[:6]
+        assert lay["bucket"] == (0, total) and total == off[6]
+        assert all(o % 64 == 0 for o in off)
+        for a, b in zip(names, names[1:]):  # blocks do not overlap
+            assert lay[a][0] + lay[a][1] * P <= lay[b][0]
+        assert lay["dsegments"][0] + 2 * P <= total < lay["dsegments"][0] + 2 * P + 64
+        assert lay["dmeans2D"][0] == total and lay["total"][1] >= lay["dcov3D"][0] + 6 * P
