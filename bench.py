@@ -16,6 +16,9 @@ Prints ONE JSON line on rank 0.  Extra objects:
                   bytes per launch from profiles/ when a counter profile exists;
                   `valu_issue_frac` = PMC SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x
                   2.4 GHz x launch time): the bound the render kernels actually hit.
+  train_step   -- (N = 1) the s8f training step around the rasterizer: fused Adam
+                  step / activation backward kernels vs the reference's torch
+                  optimizer + activations on the same GPU (gsr_tools/train_bench.py).
   cpu_baseline -- the CPU oracle (C++ restatement of the reference kernels,
                   OpenMP) timed on this box's host cores on a bounded sample of the
                   same workload (whole views, rank 0, N = 1 only).
@@ -100,6 +103,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work for cpu_baseline")
     ap.add_argument("--stages", action="store_true", help="print the per-stage table to stderr")
+    ap.add_argument("--no-train", action="store_true", help="skip the train_step measurement (SURVEY.md s8f)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -243,6 +247,10 @@ def main():
         "roofline": roof,
         "stages": stages,
     }
+    out["train_step"] = None
+    if rank == 0 and world == 1 and not args.no_train:
+        from gsr_tools import train_bench
+        out["train_step"] = train_bench.measure(scene_cpu, cam_cpu, ups, device)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(scene_cpu, cam_cpu, ups_cpu, args.cpu_budget)
     else:
