@@ -193,6 +193,7 @@ int gsr_set_option(const char* name, long long value) {
         gsr::set_sort_lookback_max(value < 0 ? 0 : (size_t)value);
         return 0;
     }
+    if (gsr::set_train_option(name, value) == 0) return 0;
     return fail(std::string("[gsr] unknown option ") + name);
 }
 

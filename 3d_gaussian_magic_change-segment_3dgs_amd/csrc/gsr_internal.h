@@ -12,6 +12,8 @@ namespace gsr {
 
 // Sets the thread-local gsr_last_error() message; returns 1 (api.hip).
 int set_error(const std::string& msg);
+// Training-kernel launch options (train.hip); -1 = unknown name.
+int set_train_option(const std::string& name, long long value);
 
 constexpr int BX = GSR_BLOCK_X, BY = GSR_BLOCK_Y;
 constexpr int NCH = GSR_NUM_CHANNELS, NCLS = GSR_NUM_CLASS;

@@ -24,6 +24,13 @@ namespace {
 constexpr int TR_THREADS = 256;
 constexpr int TR_MAX_BLOCKS = 256 * 32;  // grid-stride beyond this (8192 workgroups)
 
+// Adam launch shape (gsr_set_option "adam_items" / "adam_nt" / "adam_grid").
+// Measured at P = 1M, SH3 (tools/adam_variants.py): 4 items + non-temporal + no cap
+// = 0.289 ms (6.05 TB/s); 1 item, temporal, 8192-WG cap = 0.316 ms.
+int g_adam_items = 4;        // float4 items per thread per grid-stride iteration
+int g_adam_nt = 1;           // non-temporal loads/stores (every byte is touched once)
+long long g_adam_grid = 0;   // workgroup cap (0 = no cap: each thread does `items` items)
+
 inline long long arena_align(long long n) { return (n + GSR_ARENA_ALIGN - 1) / GSR_ARENA_ALIGN * GSR_ARENA_ALIGN; }
 
 // Float4 work map of an arena: block b covers float4 items [c4[b], c4[b+1]).
@@ -145,51 +152,84 @@ __device__ __forceinline__ void adam1(float& p, float& m, float& v, float g, flo
     p = p + ss * (m / den);                // param.addcdiv_(exp_avg, denom, value=-step_size)
 }
 
+typedef float v4f __attribute__((ext_vector_type(4)));
+template <bool NT>
+__device__ __forceinline__ float4 ld4(const float* p) {
+    if constexpr (NT) {
+        const v4f r = __builtin_nontemporal_load(reinterpret_cast<const v4f*>(p));
+        return make_float4(r.x, r.y, r.z, r.w);
+    } else {
+        return *reinterpret_cast<const float4*>(p);
+    }
+}
+template <bool NT>
+__device__ __forceinline__ void st4(float* p, float4 v) {
+    if constexpr (NT) {
+        const v4f r = {v.x, v.y, v.z, v.w};
+        __builtin_nontemporal_store(r, reinterpret_cast<v4f*>(p));
+    } else {
+        *reinterpret_cast<float4*>(p) = v;
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ void adam_item(const ArenaMap& am, const AdamArgs& a, int w, float* __restrict__ param,
+                                          const float* __restrict__ grad, float* __restrict__ exp_avg,
+                                          float* __restrict__ exp_avg_sq, float* __restrict__ act) {
+    const int b = block_of(am, w);
+    const int wl = w - am.c4[b];
+    const long long e = am.off[b] + 4LL * wl;
+    float4 p = ld4<NT>(param + e);
+    const float4 g = ld4<NT>(grad + e);
+    const float4 m = ld4<NT>(exp_avg + e);
+    const float4 v = ld4<NT>(exp_avg_sq + e);
+    float pe[4] = {p.x, p.y, p.z, p.w}, me[4] = {m.x, m.y, m.z, m.w}, ve[4] = {v.x, v.y, v.z, v.w};
+    const float ge[4] = {g.x, g.y, g.z, g.w};
+    if (b == 1) {  // features: coefficient 0 of each Gaussian is f_dc, the rest f_rest
+        int col = (4 * wl) % am.M3;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool dc = col < 3;
+            const int grp = dc ? 1 : 2;
+            if (!a.skip[grp]) adam1(pe[j], me[j], ve[j], ge[j], dc ? a.ss[1] : a.ss[2], dc ? a.bc2[1] : a.bc2[2], a);
+            col = (col + 1 == am.M3) ? 0 : col + 1;
+        }
+    } else {
+        const int grp = group_of_block(b);
+        float ss = a.ss[0], bc2 = a.bc2[0];
+        int sk = a.skip[0];
+#pragma unroll
+        for (int k = 3; k < GSR_ADAM_GROUPS; ++k) {  // select without dynamic kernarg indexing
+            if (grp == k) {
+                ss = a.ss[k];
+                bc2 = a.bc2[k];
+                sk = a.skip[k];
+            }
+        }
+        if (!sk) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) adam1(pe[j], me[j], ve[j], ge[j], ss, bc2, a);
+        }
+    }
+    p = make_float4(pe[0], pe[1], pe[2], pe[3]);
+    st4<NT>(param + e, p);
+    st4<NT>(exp_avg + e, make_float4(me[0], me[1], me[2], me[3]));
+    st4<NT>(exp_avg_sq + e, make_float4(ve[0], ve[1], ve[2], ve[3]));
+    if (act && b >= 2) st4<NT>(act + am.aoff[b - 2] + 4LL * wl, activate4(b, p));
+}
+
+template <int ITEMS, bool NT>
 __global__ void __launch_bounds__(TR_THREADS) k_adam(ArenaMap am, AdamArgs a, float* __restrict__ param,
                                                      const float* __restrict__ grad, float* __restrict__ exp_avg,
                                                      float* __restrict__ exp_avg_sq, float* __restrict__ act) {
     const int hi = am.c4[GSR_ARENA_BLOCKS];
-    for (int w = blockIdx.x * TR_THREADS + threadIdx.x; w < hi; w += gridDim.x * TR_THREADS) {
-        const int b = block_of(am, w);
-        const int wl = w - am.c4[b];
-        const long long e = am.off[b] + 4LL * wl;
-        float4 p = *reinterpret_cast<const float4*>(param + e);
-        const float4 g = *reinterpret_cast<const float4*>(grad + e);
-        float4 m = *reinterpret_cast<const float4*>(exp_avg + e);
-        float4 v = *reinterpret_cast<const float4*>(exp_avg_sq + e);
-        float pe[4] = {p.x, p.y, p.z, p.w}, me[4] = {m.x, m.y, m.z, m.w}, ve[4] = {v.x, v.y, v.z, v.w};
-        const float ge[4] = {g.x, g.y, g.z, g.w};
-        if (b == 1) {  // features: coefficient 0 of each Gaussian is f_dc, the rest f_rest
-            int col = (4 * wl) % am.M3;
+    const int nth = gridDim.x * TR_THREADS;
+    for (int w = blockIdx.x * TR_THREADS + threadIdx.x; w < hi; w += ITEMS * nth) {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                const bool dc = col < 3;
-                const int grp = dc ? 1 : 2;
-                if (!a.skip[grp]) adam1(pe[j], me[j], ve[j], ge[j], dc ? a.ss[1] : a.ss[2], dc ? a.bc2[1] : a.bc2[2], a);
-                col = (col + 1 == am.M3) ? 0 : col + 1;
-            }
-        } else {
-            const int grp = group_of_block(b);
-            float ss = a.ss[0], bc2 = a.bc2[0];
-            int sk = a.skip[0];
-#pragma unroll
-            for (int k = 3; k < GSR_ADAM_GROUPS; ++k) {  // select without dynamic kernarg indexing
-                if (grp == k) {
-                    ss = a.ss[k];
-                    bc2 = a.bc2[k];
-                    sk = a.skip[k];
-                }
-            }
-            if (!sk) {
-#pragma unroll
-                for (int j = 0; j < 4; ++j) adam1(pe[j], me[j], ve[j], ge[j], ss, bc2, a);
-            }
+        for (int k = 0; k < ITEMS; ++k) {
+            const int wk = w + k * nth;
+            if (wk < hi) adam_item<NT>(am, a, wk, param, grad, exp_avg, exp_avg_sq, act);
         }
-        p = make_float4(pe[0], pe[1], pe[2], pe[3]);
-        *reinterpret_cast<float4*>(param + e) = p;
-        *reinterpret_cast<float4*>(exp_avg + e) = make_float4(me[0], me[1], me[2], me[3]);
-        *reinterpret_cast<float4*>(exp_avg_sq + e) = make_float4(ve[0], ve[1], ve[2], ve[3]);
-        if (act && b >= 2) *reinterpret_cast<float4*>(act + am.aoff[b - 2] + 4LL * wl) = activate4(b, p);
     }
 }
 
@@ -227,6 +267,14 @@ int launched(const char* what) {
 }
 
 }  // namespace
+
+int set_train_option(const std::string& name, long long v) {
+    if (name == "adam_items") g_adam_items = (int)(v >= 4 ? 4 : v >= 2 ? 2 : 1);
+    else if (name == "adam_nt") g_adam_nt = v != 0;
+    else if (name == "adam_grid") g_adam_grid = v < 0 ? 0 : v;
+    else return -1;
+    return 0;
+}
 }  // namespace gsr
 
 using namespace gsr;
@@ -293,8 +341,23 @@ GSR_API int gsr_adam_step(int P, int M, int C, float* param, const float* grad, 
         a.skip[g] = h->skip[g];
     }
     const ArenaMap am = arena_map(P, M, C);
-    k_adam<<<grid_for(am.c4[GSR_ARENA_BLOCKS]), TR_THREADS, 0, (hipStream_t)stream>>>(am, a, param, grad, exp_avg,
-                                                                                       exp_avg_sq, act);
+    const long long items = am.c4[GSR_ARENA_BLOCKS];
+    long long blocks = (items + (long long)TR_THREADS * g_adam_items - 1) / ((long long)TR_THREADS * g_adam_items);
+    if (g_adam_grid > 0 && blocks > g_adam_grid) blocks = g_adam_grid;
+    if (blocks < 1) blocks = 1;
+    hipStream_t st = (hipStream_t)stream;
+    const dim3 grid((unsigned)blocks);
+#define GSR_ADAM_LAUNCH(IT, NT) k_adam<IT, NT><<<grid, TR_THREADS, 0, st>>>(am, a, param, grad, exp_avg, exp_avg_sq, act)
+    if (g_adam_nt) {
+        if (g_adam_items >= 4) GSR_ADAM_LAUNCH(4, true);
+        else if (g_adam_items == 2) GSR_ADAM_LAUNCH(2, true);
+        else GSR_ADAM_LAUNCH(1, true);
+    } else {
+        if (g_adam_items >= 4) GSR_ADAM_LAUNCH(4, false);
+        else if (g_adam_items == 2) GSR_ADAM_LAUNCH(2, false);
+        else GSR_ADAM_LAUNCH(1, false);
+    }
+#undef GSR_ADAM_LAUNCH
     return launched("adam_step");
 }
 
