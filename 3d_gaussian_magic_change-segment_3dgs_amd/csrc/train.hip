@@ -248,6 +248,185 @@ __global__ void __launch_bounds__(TR_THREADS) k_densify_stats(int P, const uint8
     }
 }
 
+
+// ---- densification / pruning (gaussian_model.py:386-521) ---------------------------
+// Plan: one classification pass writes four 0/1 category arrays (kept original,
+// kept clone, kept split child, split-selected), four inclusive scans turn them into
+// stable output ranks, and the apply pass moves every Gaussian to its slot(s).
+
+struct DensifyWs {
+    uint32_t* cat;   // [4][P] category flags
+    uint32_t* rank;  // [4][P] inclusive scans of cat
+    void* scan[4];   // scan workspaces
+    uint32_t* totals;  // [4]
+};
+inline size_t densify_cat_bytes(size_t P) { return align_up(4 * P * 4); }
+inline size_t densify_ws_size(size_t P) {
+    return 2 * densify_cat_bytes(P) + 4 * align_up(scan_ws_bytes(P)) + ALIGN;
+}
+inline DensifyWs densify_ws(size_t P, void* p) {
+    char* c = static_cast<char*>(p);
+    DensifyWs w;
+    w.cat = reinterpret_cast<uint32_t*>(c);
+    w.rank = reinterpret_cast<uint32_t*>(c + densify_cat_bytes(P));
+    size_t o = 2 * densify_cat_bytes(P);
+    for (int k = 0; k < 4; ++k) {
+        w.scan[k] = c + o;
+        o += align_up(scan_ws_bytes(P));
+    }
+    w.totals = reinterpret_cast<uint32_t*>(c + o);
+    return w;
+}
+
+struct DensifyK {
+    int mode, split_n;
+    float max_grad, min_opacity, clone_max_scale, prune_max_scale, max_screen_size, inv_split_div;
+};
+
+__device__ __forceinline__ float max3(const float* s) { return fmaxf(fmaxf(s[0], s[1]), s[2]); }
+
+__global__ void __launch_bounds__(TR_THREADS) k_densify_classify(ArenaMap am, int P, DensifyK d,
+                                                                 const float* __restrict__ act,
+                                                                 const float* __restrict__ accum,
+                                                                 const float* __restrict__ denom,
+                                                                 const uint8_t* __restrict__ mask,
+                                                                 uint32_t* __restrict__ cat) {
+    const int i = blockIdx.x * TR_THREADS + threadIdx.x;
+    if (i >= P) return;
+    uint32_t keep = 0, clone = 0, child = 0, split = 0;
+    if (d.mode == GSR_PRUNE_MASK) {
+        keep = mask[i] ? 0u : 1u;
+    } else {
+        float g = accum[i] / denom[i];  // grads = xyz_gradient_accum / denom; grads[isnan] = 0
+        if (g != g) g = 0.0f;
+        const float* s = act + am.aoff[1] + 3LL * i;  // get_scaling
+        const float smax = max3(s);
+        const bool sel = g >= d.max_grad;
+        const bool c = sel && smax <= d.clone_max_scale;  // densify_and_clone (:441-444)
+        const bool sp = sel && smax > d.clone_max_scale;  // densify_and_split (:408-411)
+        if (d.mode == GSR_CLONE_ONLY) {
+            keep = 1;
+            clone = c;
+        } else if (d.mode == GSR_SPLIT_ONLY) {
+            keep = !sp;
+            child = sp;
+            split = sp;
+        } else {
+            // final prune (:510-516) on the grown set: opacity, world size, and the
+            // screen size read from max_radii2D = 0 after densification_postfix
+            const float op = act[am.aoff[0] + i];
+            const bool mss = d.max_screen_size > 0.0f;
+            const bool vs = mss && (0.0f > d.max_screen_size);
+            const bool prune_o = op < d.min_opacity || vs || (mss && smax > d.prune_max_scale);
+            // children: scaling = log(s / (0.8 N)); torch divides by a scalar as a
+            // multiply by its float reciprocal
+            float cmax = 0.0f;
+            for (int k = 0; k < 3; ++k) cmax = fmaxf(cmax, expf(logf(s[k] * d.inv_split_div)));
+            const bool prune_c = op < d.min_opacity || vs || (mss && cmax > d.prune_max_scale);
+            keep = !sp && !prune_o;
+            clone = c && !prune_o;
+            child = sp && !prune_c;
+            split = sp;
+        }
+    }
+    cat[i] = keep;
+    cat[(size_t)P + i] = clone;
+    cat[2 * (size_t)P + i] = child;
+    cat[3 * (size_t)P + i] = split;
+}
+
+__global__ void k_densify_totals(const uint32_t* __restrict__ rank, int P, uint32_t* __restrict__ totals) {
+    const int k = threadIdx.x;
+    if (k < 4) totals[k] = P > 0 ? rank[(size_t)k * P + (P - 1)] : 0u;
+}
+
+// Copy Gaussian i of (src, old layout) to slot j of (dst, new layout); moments too
+// (zeroed when !keep_moments).
+__device__ __forceinline__ void copy_gaussian(const ArenaMap& so, const ArenaMap& dn, int i, int j,
+                                              const float* __restrict__ src, float* __restrict__ dst) {
+    for (int k = 0; k < 3; ++k) dst[dn.off[0] + 3LL * j + k] = src[so.off[0] + 3LL * i + k];
+    for (int k = 0; k < so.M3; ++k) dst[dn.off[1] + (long long)so.M3 * j + k] = src[so.off[1] + (long long)so.M3 * i + k];
+    dst[dn.off[2] + j] = src[so.off[2] + i];
+    for (int k = 0; k < 3; ++k) dst[dn.off[3] + 3LL * j + k] = src[so.off[3] + 3LL * i + k];
+    for (int k = 0; k < 4; ++k) dst[dn.off[4] + 4LL * j + k] = src[so.off[4] + 4LL * i + k];
+}
+__device__ __forceinline__ void copy_segments(const ArenaMap& so, const ArenaMap& dn, int C, int i, int j,
+                                              const float* __restrict__ src, float* __restrict__ dst) {
+    for (int k = 0; k < C; ++k) dst[dn.off[5] + (long long)C * j + k] = src[so.off[5] + (long long)C * i + k];
+}
+__device__ __forceinline__ void zero_gaussian(const ArenaMap& dn, int C, int j, float* __restrict__ dst) {
+    for (int k = 0; k < 3; ++k) dst[dn.off[0] + 3LL * j + k] = 0.0f;
+    for (int k = 0; k < dn.M3; ++k) dst[dn.off[1] + (long long)dn.M3 * j + k] = 0.0f;
+    dst[dn.off[2] + j] = 0.0f;
+    for (int k = 0; k < 3; ++k) dst[dn.off[3] + 3LL * j + k] = 0.0f;
+    for (int k = 0; k < 4; ++k) dst[dn.off[4] + 4LL * j + k] = 0.0f;
+    for (int k = 0; k < C; ++k) dst[dn.off[5] + (long long)C * j + k] = 0.0f;
+}
+
+__global__ void __launch_bounds__(TR_THREADS) k_densify_apply(
+    ArenaMap so, ArenaMap dn, int P, int C, DensifyK d, int base_clone, int base_child, int n_child, int n_split,
+    const uint32_t* __restrict__ cat, const uint32_t* __restrict__ rank, const float* __restrict__ param,
+    const float* __restrict__ act, const float* __restrict__ m1, const float* __restrict__ m2,
+    const float* __restrict__ normals, float* __restrict__ np, float* __restrict__ nm1, float* __restrict__ nm2) {
+    const int i = blockIdx.x * TR_THREADS + threadIdx.x;
+    if (i >= P) return;
+    const size_t P_ = (size_t)P;
+    if (cat[i]) {  // kept original: parameters and moments move
+        const int j = (int)rank[i] - 1;
+        copy_gaussian(so, dn, i, j, param, np);
+        copy_segments(so, dn, C, i, j, param, np);
+        copy_gaussian(so, dn, i, j, m1, nm1);
+        copy_segments(so, dn, C, i, j, m1, nm1);
+        copy_gaussian(so, dn, i, j, m2, nm2);
+        copy_segments(so, dn, C, i, j, m2, nm2);
+    }
+    if (cat[P_ + i]) {  // kept clone: parameters copied, fresh moments
+        const int j = base_clone + (int)rank[P_ + i] - 1;
+        copy_gaussian(so, dn, i, j, param, np);
+        copy_segments(so, dn, C, i, j, param, np);
+        zero_gaussian(dn, C, j, nm1);
+        zero_gaussian(dn, C, j, nm2);
+    }
+    if (cat[2 * P_ + i]) {  // kept split children
+        const int r = (int)rank[3 * P_ + i] - 1;  // rank among all split-selected (normals row)
+        const float* s = act + so.aoff[1] + 3LL * i;
+        const float* q = param + so.off[4] + 4LL * i;
+        // build_rotation (utils/general_utils.py:86-107): separately rounded torch ops
+        const float nrm = __fsqrt_rn(__fadd_rn(__fadd_rn(__fadd_rn(__fmul_rn(q[0], q[0]), __fmul_rn(q[1], q[1])),
+                                                         __fmul_rn(q[2], q[2])), __fmul_rn(q[3], q[3])));
+        const float w = __fdiv_rn(q[0], nrm), x = __fdiv_rn(q[1], nrm), y = __fdiv_rn(q[2], nrm),
+                    z = __fdiv_rn(q[3], nrm);
+        auto two = [](float v) { return __fmul_rn(2.0f, v); };
+        const float R[9] = {
+            __fsub_rn(1.0f, two(__fadd_rn(__fmul_rn(y, y), __fmul_rn(z, z)))),
+            two(__fsub_rn(__fmul_rn(x, y), __fmul_rn(w, z))),
+            two(__fadd_rn(__fmul_rn(x, z), __fmul_rn(w, y))),
+            two(__fadd_rn(__fmul_rn(x, y), __fmul_rn(w, z))),
+            __fsub_rn(1.0f, two(__fadd_rn(__fmul_rn(x, x), __fmul_rn(z, z)))),
+            two(__fsub_rn(__fmul_rn(y, z), __fmul_rn(w, x))),
+            two(__fsub_rn(__fmul_rn(x, z), __fmul_rn(w, y))),
+            two(__fadd_rn(__fmul_rn(y, z), __fmul_rn(w, x))),
+            __fsub_rn(1.0f, two(__fadd_rn(__fmul_rn(x, x), __fmul_rn(y, y)))),
+        };
+        for (int c = 0; c < d.split_n; ++c) {
+            const int j = base_child + c * n_child + (int)rank[2 * P_ + i] - 1;
+            const float* zr = normals + 3LL * ((long long)c * n_split + r);
+            const float smp[3] = {__fmul_rn(zr[0], s[0]), __fmul_rn(zr[1], s[1]), __fmul_rn(zr[2], s[2])};
+            copy_gaussian(so, dn, i, j, param, np);
+            copy_segments(so, dn, C, i, j, param, np);
+            for (int k = 0; k < 3; ++k) {  // bmm(R, samples) + xyz
+                float acc = __fmul_rn(R[3 * k], smp[0]);
+                acc = __fmaf_rn(R[3 * k + 1], smp[1], acc);
+                acc = __fmaf_rn(R[3 * k + 2], smp[2], acc);
+                np[dn.off[0] + 3LL * j + k] = __fadd_rn(acc, param[so.off[0] + 3LL * i + k]);
+                np[dn.off[3] + 3LL * j + k] = logf(__fmul_rn(s[k], d.inv_split_div));
+            }
+            zero_gaussian(dn, C, j, nm1);
+            zero_gaussian(dn, C, j, nm2);
+        }
+    }
+}
+
 int grid_for(long long items) {
     const long long g = (items + TR_THREADS - 1) / TR_THREADS;
     return (int)(g < 1 ? 1 : g > TR_MAX_BLOCKS ? TR_MAX_BLOCKS : g);
@@ -370,6 +549,78 @@ GSR_API int gsr_densify_stats(int P, const uint8_t* filter, const int* radii, co
     k_densify_stats<<<grid_for(P), TR_THREADS, 0, (hipStream_t)stream>>>(P, filter, radii, dmeans2D, max_radii2D,
                                                                          grad_accum, denom);
     return launched("densify_stats");
+}
+
+
+GSR_API size_t gsr_densify_ws_bytes(int P) { return densify_ws_size(P > 0 ? (size_t)P : 1); }
+
+namespace {
+DensifyK densify_k(const gsr_densify_args* a) {
+    DensifyK d{};
+    d.mode = a->mode;
+    d.split_n = a->split_n;
+    d.max_grad = a->max_grad;
+    d.min_opacity = a->min_opacity;
+    d.clone_max_scale = a->clone_max_scale;
+    d.prune_max_scale = a->prune_max_scale;
+    d.max_screen_size = a->max_screen_size;
+    d.inv_split_div = 1.0f / a->split_divisor;
+    return d;
+}
+}  // namespace
+
+GSR_API int gsr_densify_plan(int P, int M, int C, const float* param, const float* act, const float* grad_accum,
+                             const float* denom, const uint8_t* mask, const gsr_densify_args* a, void* ws,
+                             int* counts, void* stream) {
+    (void)param;
+    if (int rc = check_sizes(P, M, C)) return rc;
+    if (!a || !counts) return set_error("[gsr] gsr_densify_plan: null args/counts");
+    if (a->mode < GSR_DENSIFY_AND_PRUNE || a->mode > GSR_SPLIT_ONLY) return set_error("[gsr] densify: bad mode");
+    if (a->split_n < 1 || a->split_n > 16 || !(a->split_divisor > 0.0f))
+        return set_error("[gsr] densify: split_n must be 1..16 with a positive divisor");
+    for (int k = 0; k < 4; ++k) counts[k] = 0;
+    if (P == 0) return 0;
+    if (!ws) return set_error("[gsr] gsr_densify_plan: null workspace");
+    if (a->mode == GSR_PRUNE_MASK ? !mask : (!act || !grad_accum || !denom))
+        return set_error("[gsr] gsr_densify_plan: null input");
+    hipStream_t st = (hipStream_t)stream;
+    const ArenaMap am = arena_map(P, M, C);
+    const DensifyWs w = densify_ws(P, ws);
+    k_densify_classify<<<(P + TR_THREADS - 1) / TR_THREADS, TR_THREADS, 0, st>>>(am, P, densify_k(a), act,
+                                                                                grad_accum, denom, mask, w.cat);
+    for (int k = 0; k < 4; ++k)
+        launch_scan_inclusive_gather(w.cat + (size_t)k * P, nullptr, w.rank + (size_t)k * P, P, w.scan[k],
+                                     /*ws_zeroed=*/false, st, nullptr);
+    k_densify_totals<<<1, 64, 0, st>>>(w.rank, P, w.totals);
+    uint32_t host[4] = {0, 0, 0, 0};
+    hipError_t e = hipMemcpyAsync(host, w.totals, sizeof(host), hipMemcpyDeviceToHost, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    if (e != hipSuccess) return set_error(std::string("[gsr] densify plan: ") + hipGetErrorString(e));
+    const long long np = (long long)host[0] + host[1] + (long long)a->split_n * host[2];
+    if (np >= (1LL << 31)) return set_error("[gsr] densify: result too large");
+    for (int k = 0; k < 4; ++k) counts[k] = (int)host[k];
+    return 0;
+}
+
+GSR_API int gsr_densify_apply(int P, int M, int C, const float* param, const float* act, const float* exp_avg,
+                              const float* exp_avg_sq, const gsr_densify_args* a, const void* ws, const int* counts,
+                              const float* normals, float* new_param, float* new_exp_avg, float* new_exp_avg_sq,
+                              void* stream) {
+    if (int rc = check_sizes(P, M, C)) return rc;
+    if (!a || !counts) return set_error("[gsr] gsr_densify_apply: null args/counts");
+    const long long np = (long long)counts[0] + counts[1] + (long long)a->split_n * counts[2];
+    if (int rc = check_sizes((int)np, M, C)) return rc;
+    if (P == 0 || np == 0) return 0;
+    if (!ws || !param || !act || !exp_avg || !exp_avg_sq || !new_param || !new_exp_avg || !new_exp_avg_sq)
+        return set_error("[gsr] gsr_densify_apply: null buffer");
+    if (counts[2] > 0 && !normals) return set_error("[gsr] gsr_densify_apply: split children need normals");
+    hipStream_t st = (hipStream_t)stream;
+    const ArenaMap so = arena_map(P, M, C), dn = arena_map((int)np, M, C);
+    const DensifyWs w = densify_ws(P, const_cast<void*>(ws));
+    k_densify_apply<<<(P + TR_THREADS - 1) / TR_THREADS, TR_THREADS, 0, st>>>(
+        so, dn, P, C, densify_k(a), counts[0], counts[0] + counts[1], counts[2], counts[3], w.cat, w.rank, param, act,
+        exp_avg, exp_avg_sq, normals, new_param, new_exp_avg, new_exp_avg_sq);
+    return launched("densify_apply");
 }
 
 }  // extern "C"

@@ -32,8 +32,28 @@ _lib.gsr_adam_step.argtypes = [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, ctypes.POINT
 _lib.gsr_densify_stats.restype = _i
 _lib.gsr_densify_stats.argtypes = [_i, _vp, _vp, _vp, _vp, _vp, _vp, _vp]
 
+DENSIFY_AND_PRUNE, PRUNE_MASK, CLONE_ONLY, SPLIT_ONLY = 0, 1, 2, 3
+
+
+class DensifyArgs(ctypes.Structure):
+    _fields_ = [("mode", ctypes.c_int), ("split_n", ctypes.c_int), ("max_grad", ctypes.c_float),
+                ("min_opacity", ctypes.c_float), ("clone_max_scale", ctypes.c_float),
+                ("prune_max_scale", ctypes.c_float), ("max_screen_size", ctypes.c_float),
+                ("split_divisor", ctypes.c_float)]
+
+
+_lib.gsr_densify_ws_bytes.restype = ctypes.c_size_t
+_lib.gsr_densify_ws_bytes.argtypes = [_i]
+_lib.gsr_densify_plan.restype = _i
+_lib.gsr_densify_plan.argtypes = [_i, _i, _i, _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(DensifyArgs), _vp,
+                                  ctypes.POINTER(_i), _vp]
+_lib.gsr_densify_apply.restype = _i
+_lib.gsr_densify_apply.argtypes = [_i, _i, _i, _vp, _vp, _vp, _vp, ctypes.POINTER(DensifyArgs), _vp,
+                                   ctypes.POINTER(_i), _vp, _vp, _vp, _vp, _vp]
+
 EXPORTED_SYMBOLS = ("gsr_arena_layout", "gsr_act_layout", "gsr_activate", "gsr_activation_backward",
-                    "gsr_adam_step", "gsr_densify_stats")
+                    "gsr_adam_step", "gsr_densify_stats", "gsr_densify_ws_bytes", "gsr_densify_plan",
+                    "gsr_densify_apply")
 
 
 class ArenaSpec:
@@ -118,3 +138,37 @@ def densify_stats(dmeans2D, grad_accum, denom, update_filter=None, radii=None, m
     ptr = lambda t: None if t is None else t.data_ptr()
     _check(_lib.gsr_densify_stats(P, ptr(update_filter), ptr(radii), dmeans2D.data_ptr(), ptr(max_radii2D),
                                   grad_accum.data_ptr(), denom.data_ptr(), _stream(dev)))
+
+
+def densify(spec, param, act, exp_avg, exp_avg_sq, args, grad_accum=None, denom=None, mask=None, normals_fn=None):
+    """gsr_densify_plan + gsr_densify_apply.  normals_fn(n) returns the [n, 3]
+    standard-normal draws for the split children (called between the two, after
+    the host learns how many are needed).  Returns (new P, new param, new exp_avg,
+    new exp_avg_sq, counts)."""
+    P = spec.P
+    dev = param.device
+    ws = torch.empty(max(1, int(_lib.gsr_densify_ws_bytes(P))), dtype=torch.uint8, device=dev)
+    counts = (_i * 4)()
+    ptr = lambda t: None if t is None else t.data_ptr()
+    _check(_lib.gsr_densify_plan(P, spec.M, spec.C, param.data_ptr(), act.data_ptr(), ptr(grad_accum), ptr(denom),
+                                 ptr(mask), ctypes.byref(args), ws.data_ptr(), counts, _stream(dev)))
+    c = [int(x) for x in counts]
+    n_new = c[0] + c[1] + args.split_n * c[2]
+    normals = None
+    if c[3] > 0 and normals_fn is not None:
+        normals = normals_fn(args.split_n * c[3])
+        if normals.shape != (args.split_n * c[3], 3) or normals.dtype != torch.float32 or \
+                not normals.is_contiguous() or normals.device != dev:
+            raise RuntimeError("densify: normals must be a contiguous float32 [split_n * n_split, 3] device tensor")
+    elif c[2] > 0:
+        raise RuntimeError("densify: split children need normal draws")
+    new = ArenaSpec(n_new, spec.M, spec.C)
+    f32 = dict(dtype=torch.float32, device=dev)
+    np_, m1, m2 = (torch.empty(new.total, **f32) for _ in range(3))
+    if new.total:  # padding and any block tail are defined (zero) for the float4 kernels
+        for t in (np_, m1, m2):
+            t.zero_()
+    _check(_lib.gsr_densify_apply(P, spec.M, spec.C, param.data_ptr(), act.data_ptr(), exp_avg.data_ptr(),
+                                  exp_avg_sq.data_ptr(), ctypes.byref(args), ws.data_ptr(), counts, ptr(normals),
+                                  np_.data_ptr(), m1.data_ptr(), m2.data_ptr(), _stream(dev)))
+    return new, np_, m1, m2, c

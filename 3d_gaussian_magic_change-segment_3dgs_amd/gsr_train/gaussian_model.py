@@ -282,6 +282,78 @@ class GaussianModel:
             self.optimizer._reset_group("opacity")
         self._params_changed()
 
+    # ---- densification (gaussian_model.py:386-521) ---------------------------------------
+    def _densify_args(self, mode, max_grad=0.0, min_opacity=0.0, extent=0.0, max_screen_size=None, N=2):
+        a = _C.DensifyArgs()
+        a.mode, a.split_n = mode, int(N)
+        a.max_grad, a.min_opacity = float(max_grad), float(min_opacity)
+        a.clone_max_scale = float(self.percent_dense * extent)
+        a.prune_max_scale = float(0.1 * extent)
+        a.max_screen_size = float(max_screen_size) if max_screen_size else 0.0
+        a.split_divisor = float(0.8 * N)
+        return a
+
+    @torch.no_grad()
+    def _rebuild(self, args, grad_accum=None, denom=None, mask=None, generator=None):
+        if not self._act_fresh:
+            _C.activate(self._spec, self._arena.data, self._act)
+            self._act_fresh = True
+        opt = self.optimizer
+        m1 = opt.exp_avg if opt is not None else torch.zeros_like(self._arena.data)
+        m2 = opt.exp_avg_sq if opt is not None else torch.zeros_like(self._arena.data)
+
+        def normals(n):  # torch.normal(mean=0, std=s) draws z ~ N(0,1) as normal_ then scales
+            return torch.empty((n, 3), dtype=torch.float32, device=self.device).normal_(0.0, 1.0, generator=generator)
+
+        spec, p, m1n, m2n, counts = _C.densify(self._spec, self._arena.data, self._act, m1, m2, args,
+                                               grad_accum=grad_accum, denom=denom, mask=mask, normals_fn=normals)
+        self._spec = spec
+        self._arena = nn.Parameter(p)
+        self._act = torch.zeros(spec.act_total, dtype=torch.float32, device=self.device)
+        self._params_changed()
+        if opt is not None:
+            opt._resize(m1n, m2n)
+        P = spec.P
+        # densification_postfix (:402-404) resets the statistics; prune keeps the zeros
+        self.xyz_gradient_accum = torch.zeros((P, 1), dtype=torch.float32, device=self.device)
+        self.denom = torch.zeros((P, 1), dtype=torch.float32, device=self.device)
+        self.max_radii2D = torch.zeros(P, dtype=torch.float32, device=self.device)
+        return counts
+
+    def densify_and_prune(self, max_grad, min_opacity, extent, max_screen_size, generator=None):
+        """gaussian_model.py:508-521: clone, split (N = 2) and prune in one plan +
+        apply pair of kernels; new Gaussians get zero Adam moments."""
+        a = self._densify_args(_C.DENSIFY_AND_PRUNE, max_grad, min_opacity, extent, max_screen_size)
+        return self._rebuild(a, self.xyz_gradient_accum.contiguous(), self.denom.contiguous(), generator=generator)
+
+    def densify_and_clone(self, grads, grad_threshold, scene_extent):
+        """gaussian_model.py:439-457 (grads: [P, 1] mean view-space gradients)."""
+        a = self._densify_args(_C.CLONE_ONLY, grad_threshold, 0.0, scene_extent)
+        g = grads.reshape(-1).to(self.device, torch.float32).contiguous()
+        return self._rebuild(a, g, torch.ones_like(g))
+
+    def densify_and_split(self, grads, grad_threshold, scene_extent, N=2, generator=None):
+        """gaussian_model.py:406-437 (selected originals are removed, N children each)."""
+        a = self._densify_args(_C.SPLIT_ONLY, grad_threshold, 0.0, scene_extent, N=N)
+        P = self.num_points
+        g = torch.zeros(P, dtype=torch.float32, device=self.device)
+        src = grads.reshape(-1).to(self.device, torch.float32)
+        g[:src.numel()] = src  # padded_grad
+        return self._rebuild(a, g, torch.ones_like(g), generator=generator)
+
+    def prune_points(self, mask):
+        """gaussian_model.py:340-357: drop mask[i] (bool [P]); moments and statistics
+        follow the kept Gaussians (statistics are kept, not reset, like the reference)."""
+        keep_stats = (self.xyz_gradient_accum, self.denom, self.max_radii2D)
+        a = self._densify_args(_C.PRUNE_MASK)
+        m = mask.reshape(-1).to(self.device, torch.bool).contiguous()
+        counts = self._rebuild(a, mask=m)
+        keep = ~m
+        self.xyz_gradient_accum = keep_stats[0][keep].contiguous()
+        self.denom = keep_stats[1][keep].contiguous()
+        self.max_radii2D = keep_stats[2][keep].contiguous()
+        return counts
+
     def construct_list_of_attributes(self):
         """gaussian_model.py:187-205: PLY vertex property names in file order."""
         names = ["x", "y", "z", "nx", "ny", "nz"]

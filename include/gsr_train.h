@@ -93,6 +93,55 @@ GSR_API int gsr_adam_step(int P, int M, int C, float* param, const float* grad, 
 GSR_API int gsr_densify_stats(int P, const uint8_t* filter, const int* radii, const float* dmeans2D,
                               float* max_radii2D, float* grad_accum, float* denom, void* stream);
 
+/* ---- densification and pruning (gaussian_model.py:386-521) as two calls around
+ * one host sync (the reference syncs too: boolean-mask indexing).
+ *
+ * gsr_densify_plan classifies every Gaussian and counts the survivors:
+ *   mode GSR_DENSIFY_AND_PRUNE  densify_and_prune(max_grad, min_opacity, extent,
+ *                               max_screen_size) -- clone small / split large
+ *                               Gaussians whose mean view-space gradient
+ *                               (grad_accum / denom, NaN -> 0) >= max_grad, then
+ *                               prune sigmoid(opacity) < min_opacity and, if
+ *                               max_screen_size > 0, world-space size
+ *                               > 0.1 * extent (the screen-size test reads
+ *                               max_radii2D after densification_postfix reset it
+ *                               to 0, as the reference does);
+ *   mode GSR_PRUNE_MASK         prune_points(mask): drop mask[i] != 0;
+ *   mode GSR_CLONE_ONLY         densify_and_clone(grads, max_grad, extent);
+ *   mode GSR_SPLIT_ONLY         densify_and_split(grads, max_grad, extent, N).
+ * counts (host int[4]) = {kept originals, kept clones, kept split children per
+ * copy, split-selected Gaussians}; the new size is c0 + c1 + split_n * c2.
+ * gsr_densify_apply then writes the new arenas in the reference's order
+ * [kept originals | kept clones | children copy 0 | ... | copy N-1] (stable):
+ * clones copy their source, children get xyz = R(q) (z * s) + xyz and
+ * scaling = log(s / (0.8 N)) with s = exp(scaling) and z the caller's standard
+ * normal draws [split_n * c3, 3] (the reference's torch.normal(0, s), which
+ * draws z with normal_(0, 1) and multiplies by s).  New Gaussians get zero Adam
+ * moments; kept ones keep theirs (cat_tensors_to_optimizer / _prune_optimizer).
+ * ws holds gsr_densify_ws_bytes(P) bytes and carries the plan to the apply. */
+#define GSR_DENSIFY_AND_PRUNE 0
+#define GSR_PRUNE_MASK 1
+#define GSR_CLONE_ONLY 2
+#define GSR_SPLIT_ONLY 3
+typedef struct gsr_densify_args {
+    int mode;
+    int split_n;             /* N of densify_and_split (2 in the reference) */
+    float max_grad;          /* densify_grad_threshold */
+    float min_opacity;
+    float clone_max_scale;   /* percent_dense * scene_extent (computed in double, rounded) */
+    float prune_max_scale;   /* 0.1 * extent */
+    float max_screen_size;   /* <= 0: None */
+    float split_divisor;     /* 0.8 * N (computed in double, rounded) */
+} gsr_densify_args;
+GSR_API size_t gsr_densify_ws_bytes(int P);
+GSR_API int gsr_densify_plan(int P, int M, int C, const float* param, const float* act, const float* grad_accum,
+                             const float* denom, const uint8_t* mask, const gsr_densify_args* a, void* ws,
+                             int* counts, void* stream);
+GSR_API int gsr_densify_apply(int P, int M, int C, const float* param, const float* act, const float* exp_avg,
+                              const float* exp_avg_sq, const gsr_densify_args* a, const void* ws, const int* counts,
+                              const float* normals, float* new_param, float* new_exp_avg, float* new_exp_avg_sq,
+                              void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -216,3 +216,99 @@ def test_densify_stats(gpu_available):
     before = m.denom.clone()
     m.add_densification_stats(vp, vis.to(DEV))
     assert torch.equal((m.denom - before).squeeze(1).cpu() > 0, vis)
+
+
+def _trained_pair(P, seed=0):
+    """GPU model + CPU oracle after two identical Adam steps (non-zero moments)."""
+    raw = raw_params(P, seed=seed)
+    g = torch.Generator().manual_seed(seed + 1)
+    raw["scaling"] = raw["scaling"] + torch.randn(P, 3, generator=g) * 0.8  # spread around the clone/split edge
+    op = torch.rand(P, 1, generator=g)
+    op[::7] = 0.002  # below min_opacity
+    raw["opacity"] = torch.logit(op)
+    m, ref = make_model(raw), make_ref(raw)
+    m.spatial_lr_scale = 1.0
+    m.training_setup(_Args)
+    ref.training_setup({gr["name"]: gr["lr"] for gr in m.optimizer.param_groups})
+    keys = ["xyz", "features", "opacity", "scaling", "rotation", "segment"]
+    for _ in range(2):
+        grads = {k: torch.randn(v.shape, generator=g) * 1e-2 for k, v in ref.activated().items()}
+        torch.autograd.backward([m.get_xyz, m.get_features, m.get_opacity, m.get_scaling, m.get_rotation,
+                                 m.get_segment], [grads[k].to(DEV) for k in keys])
+        m.optimizer.step()
+        m.optimizer.zero_grad()
+        ref.backward_from_activated(grads)
+        ref.step()
+    return m, ref, g
+
+
+def _compare_state(m, ref, what):
+    """Parameters, Adam moments and statistics in the reference's row order.  The
+    two Adam steps before already differ by fp32 rounding (GPU vs CPU), so rows are
+    compared at the Adam tolerance; statistics exactly."""
+    for name in GROUPS:
+        a, b = m.group_view(name), ref.params[name].detach()
+        assert a.shape == b.shape, f"{what} {name}: {tuple(a.shape)} vs {tuple(b.shape)}"
+        # Adam steps already differ by rounding (see test_adam_matches_torch_adam): 1e-5
+        close(a, b, 1e-5, 1e-6, f"{what} {name}")
+        st = ref.optimizer.state[ref.params[name]]
+        close(m._spec.group(m.optimizer.exp_avg, name), st["exp_avg"], 1e-5, 1e-9, f"{what} {name}.exp_avg")
+        close(m._spec.group(m.optimizer.exp_avg_sq, name), st["exp_avg_sq"], 1e-5, 1e-14,
+              f"{what} {name}.exp_avg_sq")
+    close(m.xyz_gradient_accum, ref.xyz_gradient_accum, 0, 0, f"{what} accum")
+    close(m.denom, ref.denom, 0, 0, f"{what} denom")
+    close(m.max_radii2D, ref.max_radii2D, 0, 0, f"{what} max_radii2D")
+
+
+def test_densify_and_prune_matches_reference(gpu_available):
+    from oracle.train_oracle import RefDensify
+    P = 20000
+    m, ref, g = _trained_pair(P)
+    # statistics: mean gradient ~ half above threshold, some never-visible (0/0 -> 0)
+    accum = (torch.rand(P, 1, generator=g) * 4e-4)
+    denom = torch.randint(0, 4, (P, 1), generator=g).float()
+    accum[denom == 0] = 0.0
+    m.xyz_gradient_accum.copy_(accum.to(DEV))
+    m.denom.copy_(denom.to(DEV))
+    ref.xyz_gradient_accum, ref.denom = accum.clone(), denom.clone()
+    extent, max_grad, min_op = 1.2, 2e-4 / 2, 0.005
+    gen = torch.Generator(device=DEV).manual_seed(1234)
+    counts = m.densify_and_prune(max_grad, min_op, extent, 20, generator=gen)
+    assert counts[1] > 100 and counts[3] > 100, counts  # both clones and splits happen
+    gen2 = torch.Generator(device=DEV).manual_seed(1234)
+    normals = torch.empty((2 * counts[3], 3), device=DEV).normal_(0.0, 1.0, generator=gen2).cpu()
+    RefDensify.densify_and_prune(ref, max_grad, min_op, extent, 20, _Args.percent_dense, normals)
+    assert m.num_points == ref.params["xyz"].shape[0] == counts[0] + counts[1] + 2 * counts[2]
+    _compare_state(m, ref, "densify_and_prune")
+    # the model keeps training after the rebuild (layout, optimizer views, activations)
+    with torch.no_grad():
+        close(m.get_scaling, torch.exp(ref.params["scaling"].detach()), 2e-6, 1e-12, "scaling after densify")
+    grads = {k: torch.randn(v.shape, generator=g) * 1e-2 for k, v in ref.activated().items()}
+    keys = ["xyz", "features", "opacity", "scaling", "rotation", "segment"]
+    torch.autograd.backward([m.get_xyz, m.get_features, m.get_opacity, m.get_scaling, m.get_rotation,
+                             m.get_segment], [grads[k].to(DEV) for k in keys])
+    m.optimizer.step()
+    ref.backward_from_activated(grads)
+    ref.step()
+    for name in GROUPS:
+        close(m.group_view(name), ref.params[name].detach(), 2e-5, 2e-6, f"step after densify {name}")
+
+
+def test_prune_points_and_reset_opacity(gpu_available):
+    from oracle.train_oracle import RefDensify
+    P = 5000
+    m, ref, g = _trained_pair(P, seed=4)
+    mask = torch.rand(P, generator=g) < 0.3
+    stats = torch.rand(P, 1, generator=g)
+    m.xyz_gradient_accum.copy_(stats.to(DEV))
+    ref.xyz_gradient_accum = stats.clone()
+    m.prune_points(mask.to(DEV))
+    RefDensify.prune(ref, mask)
+    _compare_state(m, ref, "prune_points")
+    m.reset_opacity()
+    with torch.no_grad():
+        op = torch.sigmoid(ref.params["opacity"])
+        new = torch.log(torch.min(op, torch.ones_like(op) * 0.01) / (1 - torch.min(op, torch.ones_like(op) * 0.01)))
+    close(m._opacity, new, 1e-5, 1e-6, "reset_opacity")
+    assert float(m._spec.group(m.optimizer.exp_avg, "opacity").abs().max()) == 0.0
+    assert float(m._spec.group(m.optimizer.exp_avg, "xyz").abs().max()) > 0.0
