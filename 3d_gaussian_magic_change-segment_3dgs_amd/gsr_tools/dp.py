@@ -45,3 +45,25 @@ def pack_arena(grads, P, M):
             o, k = lay[name]
             arena.narrow(0, o, k * P).copy_(torch.as_tensor(grads[name]).reshape(-1))
     return arena
+
+
+def allreduce_model_grad(model, group=None):
+    """Sum a gsr_train.GaussianModel's arena gradient over all ranks, in place.  The
+    arena gradient has the bucket layout, so this is the same single collective."""
+    g = model._arena.grad
+    if g is not None:
+        dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
+    return g
+
+
+def reduce_densification_stats(xyz_gradient_accum, denom, max_radii2D, group=None):
+    """Combine per-rank densification statistics before densify_and_prune
+    (SURVEY.md s8e): accumulated view-space gradient norms and view counts are
+    summed, max_radii2D is max-reduced.  Each rank accumulated its own views'
+    |dmeans2D| before any reduction, as the reference does per view."""
+    both = torch.cat([xyz_gradient_accum.reshape(-1), denom.reshape(-1)])
+    dist.all_reduce(both, op=dist.ReduceOp.SUM, group=group)
+    n = xyz_gradient_accum.numel()
+    xyz_gradient_accum.copy_(both[:n].view_as(xyz_gradient_accum))
+    denom.copy_(both[n:].view_as(denom))
+    dist.all_reduce(max_radii2D, op=dist.ReduceOp.MAX, group=group)

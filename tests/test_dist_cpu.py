@@ -73,3 +73,39 @@ def test_view_parallel_allreduce_gloo_ws2():
     for rank, b, m2d_untouched in res:
         np.testing.assert_allclose(b, ref, rtol=0, atol=1e-7)
         assert m2d_untouched, "per-view means2D gradients must not be reduced"
+
+
+def _stats_worker(rank, world, port, out_q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd")]
+    from gsr_tools import dp
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    g = torch.Generator().manual_seed(rank)
+    accum, denom = torch.rand(100, 1, generator=g), torch.randint(0, 5, (100, 1), generator=g).float()
+    radii = torch.randint(0, 50, (100,), generator=g).float()
+    dp.reduce_densification_stats(accum, denom, radii)
+    out_q.put((rank, accum.numpy().copy(), denom.numpy().copy(), radii.numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_densification_stats_reduction_gloo_ws2():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_stats_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = [None, None, None]
+    for rank in range(2):
+        g = torch.Generator().manual_seed(rank)
+        a, d = torch.rand(100, 1, generator=g), torch.randint(0, 5, (100, 1), generator=g).float()
+        r = torch.randint(0, 50, (100,), generator=g).float()
+        ref = [a, d, r] if ref[0] is None else [ref[0] + a, ref[1] + d, torch.maximum(ref[2], r)]
+    for rank, a, d, r in res:
+        np.testing.assert_allclose(a, ref[0].numpy(), rtol=1e-6)
+        assert np.array_equal(d, ref[1].numpy()) and np.array_equal(r, ref[2].numpy())
