@@ -427,6 +427,49 @@ __global__ void __launch_bounds__(TR_THREADS) k_densify_apply(
     }
 }
 
+
+// ---- PLY rows <-> arena ----------------------------------------------------------
+// One thread per (Gaussian, float).  rows_to_arena walks the arena floats of a
+// Gaussian (k) and gathers its row column; arena_to_rows walks the row columns (f)
+// and gathers the arena float, so the side that streams the most (the row store)
+// is the coalesced one.
+struct PlyMap {
+    int K;                          // arena floats per Gaussian
+    int F;                          // row floats
+    int col[GSR_PLY_MAX_COLS];      // arena float k -> row column (-1: none)
+    int inv[GSR_PLY_MAX_COLS];      // row column f -> arena float (-1: none)
+    signed char blk[GSR_PLY_MAX_COLS];  // arena float k -> block
+    unsigned char sub[GSR_PLY_MAX_COLS];  // arena float k -> index inside the Gaussian's block row
+    int width[GSR_ARENA_BLOCKS];
+};
+
+__global__ void __launch_bounds__(TR_THREADS) k_ply_rows_to_arena(ArenaMap am, PlyMap pm, int n, int dst,
+                                                                  const float* __restrict__ rows,
+                                                                  float* __restrict__ param) {
+    const long long t = (long long)blockIdx.x * TR_THREADS + threadIdx.x;
+    if (t >= (long long)n * pm.K) return;
+    const int i = (int)(t / pm.K), k = (int)(t % pm.K);
+    const int c = pm.col[k];
+    const float v = c >= 0 ? rows[(long long)i * pm.F + c] : 0.0f;
+    const int b = pm.blk[k];
+    param[am.off[b] + (long long)(dst + i) * pm.width[b] + pm.sub[k]] = v;
+}
+
+__global__ void __launch_bounds__(TR_THREADS) k_arena_to_ply_rows(ArenaMap am, PlyMap pm, int P,
+                                                                  const float* __restrict__ param,
+                                                                  float* __restrict__ rows) {
+    const long long t = (long long)blockIdx.x * TR_THREADS + threadIdx.x;
+    if (t >= (long long)P * pm.F) return;
+    const int i = (int)(t / pm.F), f = (int)(t % pm.F);
+    const int k = pm.inv[f];
+    float v = 0.0f;
+    if (k >= 0) {
+        const int b = pm.blk[k];
+        v = param[am.off[b] + (long long)i * pm.width[b] + pm.sub[k]];
+    }
+    rows[t] = v;
+}
+
 int grid_for(long long items) {
     const long long g = (items + TR_THREADS - 1) / TR_THREADS;
     return (int)(g < 1 ? 1 : g > TR_MAX_BLOCKS ? TR_MAX_BLOCKS : g);
@@ -621,6 +664,62 @@ GSR_API int gsr_densify_apply(int P, int M, int C, const float* param, const flo
         so, dn, P, C, densify_k(a), counts[0], counts[0] + counts[1], counts[2], counts[3], w.cat, w.rank, param, act,
         exp_avg, exp_avg_sq, normals, new_param, new_exp_avg, new_exp_avg_sq);
     return launched("densify_apply");
+}
+
+
+namespace {
+int ply_map(int M, int C, int row_floats, const int* col, PlyMap& pm) {
+    const int K = 3 + 3 * M + 1 + 3 + 4 + C;
+    if (K > GSR_PLY_MAX_COLS || row_floats <= 0 || row_floats > GSR_PLY_MAX_COLS || !col)
+        return set_error("[gsr] ply: too many columns or no column map");
+    pm.K = K;
+    pm.F = row_floats;
+    const int widths[GSR_ARENA_BLOCKS] = {3, 3 * M, 1, 3, 4, C};
+    for (int f = 0; f < GSR_PLY_MAX_COLS; ++f) pm.inv[f] = -1;
+    int k = 0;
+    for (int b = 0; b < GSR_ARENA_BLOCKS; ++b) {
+        pm.width[b] = widths[b];
+        for (int j = 0; j < widths[b]; ++j, ++k) {
+            const int c = col[k];
+            if (c >= row_floats) return set_error("[gsr] ply: column index out of range");
+            pm.col[k] = c < 0 ? -1 : c;
+            pm.blk[k] = (signed char)b;
+            pm.sub[k] = (unsigned char)j;
+            if (c >= 0) {
+                if (pm.inv[c] >= 0) return set_error("[gsr] ply: a row column is mapped twice");
+                pm.inv[c] = k;
+            }
+        }
+    }
+    return 0;
+}
+}  // namespace
+
+GSR_API int gsr_ply_rows_to_arena(int n, int row_floats, const float* rows, const int* col, int P, int M, int C,
+                                  int dst, float* param, void* stream) {
+    if (int rc = check_sizes(P, M, C)) return rc;
+    if (n < 0 || dst < 0 || (long long)dst + n > P) return set_error("[gsr] ply: rows do not fit the arena");
+    if (n == 0) return 0;
+    if (!rows || !param) return set_error("[gsr] ply: null buffer");
+    PlyMap pm;
+    if (int rc = ply_map(M, C, row_floats, col, pm)) return rc;
+    const long long items = (long long)n * pm.K;
+    k_ply_rows_to_arena<<<(unsigned)((items + TR_THREADS - 1) / TR_THREADS), TR_THREADS, 0, (hipStream_t)stream>>>(
+        arena_map(P, M, C), pm, n, dst, rows, param);
+    return launched("ply_rows_to_arena");
+}
+
+GSR_API int gsr_arena_to_ply_rows(int P, int M, int C, const float* param, int row_floats, const int* col,
+                                  float* rows, void* stream) {
+    if (int rc = check_sizes(P, M, C)) return rc;
+    if (P == 0) return 0;
+    if (!rows || !param) return set_error("[gsr] ply: null buffer");
+    PlyMap pm;
+    if (int rc = ply_map(M, C, row_floats, col, pm)) return rc;
+    const long long items = (long long)P * pm.F;
+    k_arena_to_ply_rows<<<(unsigned)((items + TR_THREADS - 1) / TR_THREADS), TR_THREADS, 0, (hipStream_t)stream>>>(
+        arena_map(P, M, C), pm, P, param, rows);
+    return launched("arena_to_ply_rows");
 }
 
 }  // extern "C"

@@ -20,11 +20,14 @@ train.py loop drive it unchanged.  What differs is the storage:
 Editing the raw views in place (e.g. `model._opacity.fill_(0)`) is allowed;
 call `model.invalidate()` afterwards so the activated copy is refreshed.
 """
+import os
+
 import numpy as np
 import torch
 import torch.nn as nn
 
 from . import _C
+from . import ply as _ply
 from .optim import GaussianAdam
 
 
@@ -356,14 +359,81 @@ class GaussianModel:
 
     def construct_list_of_attributes(self):
         """gaussian_model.py:187-205: PLY vertex property names in file order."""
-        names = ["x", "y", "z", "nx", "ny", "nz"]
-        names += [f"f_dc_{i}" for i in range(3)]
-        names += [f"f_rest_{i}" for i in range(3 * (self._M - 1))]
-        names.append("opacity")
-        names += [f"segment_{i}" for i in range(self.num_class)]
-        names += [f"scale_{i}" for i in range(3)]
-        names += [f"rot_{i}" for i in range(4)]
-        return names
+        return _ply.attribute_names(self._M, self.num_class)
+
+    # ---- PLY (gaussian_model.py:207-338; merge: visualizer.py:196-226) ---------------------
+    @torch.no_grad()
+    def save_ply(self, path, mask=None):
+        """Binary little-endian PLY of the raw parameters, attribute order of
+        construct_list_of_attributes (normals written as 0).  The arena -> row
+        transposition runs on the GPU; one D2H copy of the vertex block."""
+        d = os.path.dirname(path)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        names = self.construct_list_of_attributes()
+        rows = _ply.arena_to_rows(self._spec, self._arena.data, names)
+        if mask is not None:
+            rows = rows[mask.to(rows.device)]
+        _ply.write_rows(path, names, rows.cpu().numpy())
+
+    def save_ply_using_mask(self, path, mask):
+        """gaussian_model.py:226-262 (every attribute masked, segments included)."""
+        self.save_ply(path, mask=mask)
+
+    @torch.no_grad()
+    def load_ply(self, path):
+        """gaussian_model.py:270-315: one H2D copy of the vertex block, transposed
+        into the arena on the GPU; active_sh_degree = max_sh_degree."""
+        self.merge_ply([path])
+        self.active_sh_degree = self.max_sh_degree
+
+    @torch.no_grad()
+    def merge_ply(self, paths):
+        """Load several PLY scenes into one model, concatenated in order (the
+        reference's _merge_scenes, visualizer.py:196-226).  Returns
+        ([(start_offset, end_offset)] per scene, point_object_id int32 [P])."""
+        files = [_ply.read_rows(p) for p in paths]
+        P = sum(r.shape[0] for _, r in files)
+        self._allocate(P)
+        offsets, o = [], 0
+        for names, rows in files:
+            _ply.arena_columns(names, self._M, self.num_class)  # validate before any upload
+        for names, rows in files:
+            n = rows.shape[0]
+            if n:
+                dev_rows = torch.from_numpy(rows).pin_memory().to(self.device, non_blocking=True)
+                _ply.rows_to_arena(self._spec, self._arena.data, dev_rows, names, dst=o)
+            offsets.append((o, o + n))
+            o += n
+        ids = torch.zeros(P, dtype=torch.int32, device=self.device)
+        for k, (a, b) in enumerate(offsets):
+            ids[a:b] = k
+        self._params_changed()
+        self.active_sh_degree = self.max_sh_degree
+        return offsets, ids
+
+    def load_ply_no_instance(self, path):
+        """gaussian_model.py:317-352: host arrays (xyz, features_dc [P,3,1],
+        features_extra [P,3,M-1], opacities, scales, rots, segments)."""
+        names, rows = _ply.read_rows(path)
+        col = _ply.arena_columns(names, self._M, self.num_class)
+        M, C = self._M, self.num_class
+        take = lambda ks: rows[:, [col[k] for k in ks]].astype(np.float64)
+        xyz = take(range(3))
+        feats = take(range(3, 3 + 3 * M)).reshape(-1, M, 3)  # [P, M, 3]
+        o = 3 + 3 * M
+        opac = take([o])
+        scales = take(range(o + 1, o + 4))
+        rots = take(range(o + 4, o + 8))
+        segs = take(range(o + 8, o + 8 + C))
+        return (xyz, feats[:, :1].transpose(0, 2, 1), feats[:, 1:].transpose(0, 2, 1), opac, scales, rots, segs)
+
+    def instance_parm(self, xyz, features_dc, features_extra, opacities, scales, rots, segments):
+        """gaussian_model.py:354-367 (features_dc [P,3,1], features_extra [P,3,M-1])."""
+        t = lambda a: torch.as_tensor(np.asarray(a), dtype=torch.float32)
+        self.create_from_tensors(t(xyz), t(features_dc).transpose(1, 2), t(features_extra).transpose(1, 2),
+                                 t(opacities), t(segments), t(scales), t(rots))
+        self.active_sh_degree = self.max_sh_degree
 
 
 def build_rotation(r):

@@ -142,6 +142,20 @@ GSR_API int gsr_densify_apply(int P, int M, int C, const float* param, const flo
                               const float* normals, float* new_param, float* new_exp_avg, float* new_exp_avg_sq,
                               void* stream);
 
+/* ---- PLY vertex rows <-> arena (save_ply / load_ply, gaussian_model.py:207-262 and
+ * the multi-scene merge of visualizer.py:196-226).  `rows` is the file's vertex
+ * block as float32 rows of row_floats columns, on the device.  col[k] names the row
+ * column of arena float k of one Gaussian, k in arena order (xyz 3 | features 3M
+ * as [M,3] | opacity | scaling 3 | rotation 4 | segment C), -1 = not in the file
+ * (zero).  rows_to_arena writes Gaussians [dst, dst + n) of an arena sized for P
+ * (so several files merge into one arena); arena_to_rows writes every column of
+ * every row (columns no arena float maps to, e.g. the normals, become 0). */
+#define GSR_PLY_MAX_COLS 128
+GSR_API int gsr_ply_rows_to_arena(int n, int row_floats, const float* rows, const int* col, int P, int M, int C,
+                                  int dst, float* param, void* stream);
+GSR_API int gsr_arena_to_ply_rows(int P, int M, int C, const float* param, int row_floats, const int* col,
+                                  float* rows, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

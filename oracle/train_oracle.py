@@ -173,3 +173,34 @@ class RefDensify:
             big_ws = torch.exp(g.params["scaling"].detach()).max(dim=1).values > 0.1 * extent
             prune = torch.logical_or(torch.logical_or(prune, big_vs), big_ws)
         RefDensify.prune(g, prune)
+
+
+# ---- PLY (gaussian_model.py:207-224 save_ply, :270-315 load_ply) ---------------------
+# The reference writes with plyfile (absent here: parity unpinned against plyfile
+# itself; the byte layout below restates the PLY spec as plyfile emits it for an
+# all-'f4' vertex element: ascii header, `format binary_little_endian 1.0`,
+# `property float <name>` per attribute, then the packed little-endian rows).
+
+def ply_attribute_matrix(xyz, f_dc, f_rest, opacity, segment, scaling, rotation):
+    """The [P, F] float32 matrix save_ply concatenates (normals are zeros; f_dc /
+    f_rest are transposed to channel-major before flattening)."""
+    import numpy as np
+    a = lambda t: torch.as_tensor(t).detach().float().cpu()
+    P = a(xyz).shape[0]
+    fdc = a(f_dc).transpose(1, 2).flatten(start_dim=1)
+    frest = a(f_rest).transpose(1, 2).flatten(start_dim=1)
+    cols = [a(xyz), torch.zeros(P, 3), fdc, frest, a(opacity).reshape(P, 1), a(segment), a(scaling), a(rotation)]
+    return np.concatenate([c.numpy() for c in cols], axis=1).astype(np.float32)
+
+
+def ply_reference_bytes(names, matrix, fmt="binary_little_endian", prop_type="float"):
+    """Bytes of a PLY file with one vertex element (plyfile's layout)."""
+    import numpy as np
+    head = ["ply", f"format {fmt} 1.0", f"element vertex {matrix.shape[0]}"]
+    head += [f"property {prop_type} {n}" for n in names] + ["end_header"]
+    out = ("\n".join(head) + "\n").encode("ascii")
+    if fmt == "ascii":
+        return out + "".join(" ".join(repr(float(v)) for v in row) + "\n" for row in matrix).encode("ascii")
+    np_t = {"float": "f4", "double": "f8"}[prop_type]
+    end = "<" if fmt == "binary_little_endian" else ">"
+    return out + np.ascontiguousarray(matrix, dtype=end + np_t).tobytes()
