@@ -53,7 +53,8 @@ _lib.gsr_densify_apply.argtypes = [_i, _i, _i, _vp, _vp, _vp, _vp, ctypes.POINTE
 
 EXPORTED_SYMBOLS = ("gsr_arena_layout", "gsr_act_layout", "gsr_activate", "gsr_activation_backward",
                     "gsr_adam_step", "gsr_densify_stats", "gsr_densify_ws_bytes", "gsr_densify_plan",
-                    "gsr_densify_apply", "gsr_ply_rows_to_arena", "gsr_arena_to_ply_rows")
+                    "gsr_densify_apply", "gsr_ply_rows_to_arena", "gsr_arena_to_ply_rows", "gsr_knn_ws_bytes",
+                    "gsr_dist_knn3")
 
 
 class ArenaSpec:

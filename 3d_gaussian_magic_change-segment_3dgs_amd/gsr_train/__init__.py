@@ -6,3 +6,4 @@ the fused replacement of its torch.optim.Adam.  Kernels: include/gsr_train.h
 from .gaussian_model import GaussianModel, get_expon_lr_func, inverse_sigmoid, build_rotation  # noqa: F401
 from .optim import GaussianAdam  # noqa: F401
 from ._C import ArenaSpec  # noqa: F401
+from .knn import distCUDA2  # noqa: F401

@@ -210,6 +210,26 @@ class GaussianModel:
         self._params_changed()
         return self
 
+    @torch.no_grad()
+    def create_from_pcd(self, pcd, spatial_lr_scale: float):
+        """gaussian_model.py:129-156: SH DC from the point colours (RGB2SH), scales
+        from the 3-NN mean squared distance (distCUDA2 -> csrc/knn.hip), identity
+        rotations, opacity and segment logits of 0.1."""
+        from .knn import distCUDA2
+        self.spatial_lr_scale = spatial_lr_scale
+        pts = torch.as_tensor(np.asarray(pcd.points), dtype=torch.float32).to(self.device)
+        cols = torch.as_tensor(np.asarray(pcd.colors), dtype=torch.float32).to(self.device)
+        P, M = pts.shape[0], self._M
+        f_dc = ((cols - 0.5) / 0.28209479177387814).reshape(P, 1, 3)  # RGB2SH (utils/sh_utils.py:114-115)
+        f_rest = torch.zeros((P, M - 1, 3), dtype=torch.float32, device=self.device)
+        dist2 = torch.clamp_min(distCUDA2(pts), 0.0000001)
+        scales = torch.log(torch.sqrt(dist2))[..., None].repeat(1, 3)
+        rots = torch.zeros((P, 4), dtype=torch.float32, device=self.device)
+        rots[:, 0] = 1
+        opac = inverse_sigmoid(0.1 * torch.ones((P, 1), dtype=torch.float32, device=self.device))
+        segs = inverse_sigmoid(0.1 * torch.ones((P, self.num_class), dtype=torch.float32, device=self.device))
+        self.create_from_tensors(pts, f_dc, f_rest, opac, segs, scales, rots)
+
     def training_setup(self, training_args):
         """gaussian_model.py:158-177 with GaussianAdam in place of torch.optim.Adam."""
         self.percent_dense = training_args.percent_dense

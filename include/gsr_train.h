@@ -156,6 +156,12 @@ GSR_API int gsr_ply_rows_to_arena(int n, int row_floats, const float* rows, cons
 GSR_API int gsr_arena_to_ply_rows(int P, int M, int C, const float* param, int row_floats, const int* col,
                                   float* rows, void* stream);
 
+/* ---- distCUDA2 (submodules_local/simple-knn/simple_knn.cu:181-220, called at
+ * gaussian_model.py:143): mean_dists[i] = mean squared distance of point i to its
+ * 3 nearest other points (exact).  points: device [P,3]; ws: gsr_knn_ws_bytes(P). */
+GSR_API size_t gsr_knn_ws_bytes(int P);
+GSR_API int gsr_dist_knn3(int P, const float* points, float* mean_dists, void* ws, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

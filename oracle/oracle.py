@@ -57,6 +57,7 @@ def lib():
         L.oracle_set_exp_libm.argtypes = [ctypes.c_int]
         L.oracle_expf.argtypes = [ctypes.c_float]
         L.oracle_expf.restype = ctypes.c_float
+        L.oracle_dist_knn3.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
         _lib = L
     return _lib
 
@@ -199,3 +200,13 @@ def mark_visible(means3D, viewmatrix):
     if P:
         lib().oracle_mark_visible(P, _ptr(m), _ptr(v), _ptr(out))
     return out.astype(bool)
+
+
+def dist_knn3(points):
+    """distCUDA2 restated (knn_oracle.cpp): mean squared distance to the 3 nearest
+    neighbours of every point, float32 [P]."""
+    pts = np.ascontiguousarray(points, dtype=np.float32).reshape(-1, 3)
+    out = np.zeros(pts.shape[0], dtype=np.float32)
+    if pts.shape[0]:
+        lib().oracle_dist_knn3(pts.shape[0], pts.ctypes.data, out.ctypes.data)
+    return out
