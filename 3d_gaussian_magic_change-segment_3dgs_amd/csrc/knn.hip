@@ -10,11 +10,14 @@
 //   * a candidate box's points are staged once into LDS and read by every thread of
 //     the workgroup that still needs that box (ds_read broadcast), instead of each
 //     thread re-reading them from L2;
-//   * boxes are visited own box first, then outward in Morton order (b-1, b+1,
-//     b-2, ...), so the 3rd-best bound is tight after a few boxes; every other box
-//     is rejected by a point-box distance test (exact: a box farther than the
-//     current 3rd best cannot hold a neighbour), with a workgroup vote so the LDS
-//     stage is skipped when no thread needs the box.
+//   * the own box is scanned first (a tight 3rd-best bound), then groups of 64
+//     boxes ("super boxes") outward in Morton order; a super box, and then each of
+//     its boxes, is rejected for the whole workgroup when its AABB is farther from
+//     the workgroup's AABB than the largest current 3rd best (exact: such a box
+//     cannot hold a neighbour of any of its queries), and per thread by the
+//     point-box distance, with a workgroup vote so the LDS stage is skipped when
+//     no thread needs the box.  Work is ~linear in P instead of the reference's
+//     every-point-tests-every-box scan.
 // The result is the exact 3-NN mean like the reference's; squared distances are
 // d.x*d.x + d.y*d.y + d.z*d.z in fp32.
 #include <float.h>
@@ -30,6 +33,7 @@ namespace {
 constexpr int KNN_BOX = 256;
 constexpr int KNN_THREADS = 256;
 constexpr int KNN_BOUND_BLOCKS = 256;
+constexpr int KNN_SUPER = 64;  // boxes per super box (level-2 culling)
 
 __device__ __forceinline__ uint32_t spread10(uint32_t x) {
     x = (x | (x << 16)) & 0x030000FFu;
@@ -137,24 +141,57 @@ __device__ __forceinline__ void update3(float4 q, float4 p, float& b0, float& b1
     if (b2 > d) b2 = d;
 }
 
+// Squared distance between two AABBs (0 if they overlap).
+__device__ __forceinline__ float box_box_dist(float4 amn, float4 amx, float4 bmn, float4 bmx) {
+    const float dx = fmaxf(0.0f, fmaxf(amn.x - bmx.x, bmn.x - amx.x));
+    const float dy = fmaxf(0.0f, fmaxf(amn.y - bmx.y, bmn.y - amx.y));
+    const float dz = fmaxf(0.0f, fmaxf(amn.z - bmx.z, bmn.z - amx.z));
+    return dx * dx + dy * dy + dz * dz;
+}
+
+__device__ __forceinline__ float wave_max(float v) {
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+// AABBs of KNN_SUPER consecutive boxes (one thread per super box).
+__global__ void k_knn_super(int nbox, const float4* __restrict__ boxes, float4* __restrict__ sup) {
+    const int sidx = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lo = sidx * KNN_SUPER;
+    if (lo >= nbox) return;
+    float4 mn = boxes[2 * lo], mx = boxes[2 * lo + 1];
+    for (int c = lo + 1; c < min(nbox, lo + KNN_SUPER); ++c) {
+        const float4 a = boxes[2 * c], z = boxes[2 * c + 1];
+        mn = make_float4(fminf(mn.x, a.x), fminf(mn.y, a.y), fminf(mn.z, a.z), 0.0f);
+        mx = make_float4(fmaxf(mx.x, z.x), fmaxf(mx.y, z.y), fmaxf(mx.z, z.z), 0.0f);
+    }
+    sup[2 * sidx] = mn;
+    sup[2 * sidx + 1] = mx;
+}
+
 __global__ void __launch_bounds__(KNN_THREADS) k_knn_query(int P, int nbox, const float4* __restrict__ sp,
                                                            const float4* __restrict__ boxes,
+                                                           const float4* __restrict__ sup,
                                                            const uint32_t* __restrict__ order,
                                                            float* __restrict__ out) {
     __shared__ float4 cand[KNN_BOX];
+    __shared__ float wmax[KNN_THREADS / 64];
     const int b = blockIdx.x;
     const int i = b * KNN_BOX + threadIdx.x;
     const bool valid = i < P;
     const float4 q = valid ? sp[i] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float4 qmn = boxes[2 * b], qmx = boxes[2 * b + 1];
     float b0 = FLT_MAX, b1 = FLT_MAX, b2 = FLT_MAX;
-    // own box, then b-1, b+1, b-2, b+2, ... (Morton neighbours first)
-    const int tmax = 2 * max(b, nbox - 1 - b) + 1;
-    for (int t = 0; t < tmax; ++t) {  // uniform over the workgroup
-        const int c = (t & 1) ? b + ((t + 1) >> 1) : b - (t >> 1);
-        if (c < 0 || c >= nbox) continue;
+    float wg_thr = FLT_MAX;  // max over the workgroup's 3rd-best distances (uniform)
+
+    // Scan box c (uniform call): stage it in LDS if any thread may find a neighbour.
+    auto visit = [&](int c) {
         const float4 mn = boxes[2 * c], mx = boxes[2 * c + 1];
+        // uniform rejection: no point of this box is nearer to any of our queries
+        // than that query's current 3rd best
+        if (box_box_dist(qmn, qmx, mn, mx) > wg_thr) return;
         const bool need = valid && box_dist(mn, mx, q) <= b2;
-        if (!__syncthreads_or(need)) continue;
+        if (!__syncthreads_or(need)) return;
         const int base = c * KNN_BOX;
         const int n = min(KNN_BOX, P - base);
         if ((int)threadIdx.x < n) cand[threadIdx.x] = sp[base + threadIdx.x];
@@ -164,7 +201,24 @@ __global__ void __launch_bounds__(KNN_THREADS) k_knn_query(int P, int nbox, cons
             for (int j = 0; j < n; ++j)
                 if (j != self) update3(q, cand[j], b0, b1, b2);
         }
+        const float m = wave_max(valid ? b2 : 0.0f);
+        if ((threadIdx.x & 63) == 0) wmax[threadIdx.x >> 6] = m;
         __syncthreads();
+        wg_thr = fmaxf(fmaxf(wmax[0], wmax[1]), fmaxf(wmax[2], wmax[3]));
+        __syncthreads();
+    };
+
+    visit(b);  // own box first: a tight bound for everything after
+    // then super boxes outward in Morton order, each rejected as a whole when possible
+    const int nsup = (nbox + KNN_SUPER - 1) / KNN_SUPER, sb = b / KNN_SUPER;
+    const int tmax = 2 * max(sb, nsup - 1 - sb) + 1;
+    for (int t = 0; t < tmax; ++t) {  // uniform over the workgroup
+        const int S = (t & 1) ? sb + ((t + 1) >> 1) : sb - (t >> 1);
+        if (S < 0 || S >= nsup) continue;
+        if (box_box_dist(qmn, qmx, sup[2 * S], sup[2 * S + 1]) > wg_thr) continue;
+        const int lo = S * KNN_SUPER, hi = min(nbox, lo + KNN_SUPER);
+        for (int c = lo; c < hi; ++c)
+            if (c != b) visit(c);
     }
     if (valid) out[order[i]] = (b0 + b1 + b2) / 3.0f;
 }
@@ -172,7 +226,7 @@ __global__ void __launch_bounds__(KNN_THREADS) k_knn_query(int P, int nbox, cons
 struct KnnWs {
     float* partial;
     uint32_t *codes, *codes_tmp, *codes_sorted, *idx_tmp, *order;
-    float4 *sp, *boxes;
+    float4 *sp, *boxes, *sup;
     void* sort;
 };
 size_t knn_ws_size(size_t P, KnnWs* w, char* base) {
@@ -187,6 +241,7 @@ size_t knn_ws_size(size_t P, KnnWs* w, char* base) {
     char* order = take(P * 4);
     char* sp = take(P * 16);
     char* boxes = take(nbox * 32);
+    char* sup = take(cdiv(nbox, KNN_SUPER) * 32);
     char* sort = take(sort_ws_bytes(P, 4));
     if (w) {
         w->partial = (float*)partial;
@@ -197,6 +252,7 @@ size_t knn_ws_size(size_t P, KnnWs* w, char* base) {
         w->order = (uint32_t*)order;
         w->sp = (float4*)sp;
         w->boxes = (float4*)boxes;
+        w->sup = (float4*)sup;
         w->sort = sort;
     }
     return o;
@@ -227,7 +283,9 @@ GSR_API int gsr_dist_knn3(int P, const float* points, float* mean_dists, void* w
                       /*ws_zeroed=*/false, st);
     k_knn_gather<<<g, 256, 0, st>>>(P, points, w.order, w.sp);
     k_knn_boxes<<<nbox, KNN_THREADS, 0, st>>>(P, w.sp, w.boxes);
-    k_knn_query<<<nbox, KNN_THREADS, 0, st>>>(P, nbox, w.sp, w.boxes, w.order, mean_dists);
+    const int nsup = (int)cdiv((size_t)nbox, KNN_SUPER);
+    k_knn_super<<<(unsigned)cdiv((size_t)nsup, 64), 64, 0, st>>>(nbox, w.boxes, w.sup);
+    k_knn_query<<<nbox, KNN_THREADS, 0, st>>>(P, nbox, w.sp, w.boxes, w.sup, w.order, mean_dists);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return set_error(std::string("[gsr] dist_knn3: ") + hipGetErrorString(e));
     return 0;

@@ -127,6 +127,23 @@ def measure(scene_cpu, cam_cpu, ups, device, reps=20, iters=10):
 
     fused_iter_ms = _events_ms(fused_iter, iters)
     ref_iter_ms = _events_ms(ref_iter, iters)
+
+    # densify_and_prune once on the trained model (statistics: mean grad ~U[0, 4e-4])
+    P0 = m.num_points
+    m.xyz_gradient_accum.uniform_(0.0, 4e-4, generator=gen)
+    m.denom.fill_(1.0)
+    torch.cuda.synchronize()
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    counts = m.densify_and_prune(2e-4, 0.005, 1.5, 20, generator=gen)
+    b.record()
+    b.synchronize()
+    densify_ms = a.elapsed_time(b)
+
+    # distCUDA2 (create_from_pcd) on the scene's means
+    from gsr_train import distCUDA2
+    pts = scene_cpu.means3D.to(device)
+    knn_ms = _events_ms(lambda: distCUDA2(pts), 3)
     ab = adam_bytes(P, M)
     return {
         "workload": f"P={P}, SH{deg}, 7 param groups (scene/gaussian_model.py:162-170)",
@@ -141,4 +158,7 @@ def measure(scene_cpu, cam_cpu, ups, device, reps=20, iters=10):
         "train_iteration_ms": {"fused": round(fused_iter_ms, 4), "reference_style": round(ref_iter_ms, 4),
                                "note": "activations + rasterizer fwd+bwd (this library) + activation bwd + "
                                        "Adam step, one view"},
+        "densify_and_prune": {"ms": round(densify_ms, 3), "P_before": P0, "P_after": m.num_points,
+                              "counts": counts, "note": "plan (classify + 4 scans) + host sync + apply"},
+        "dist_knn3": {"ms": round(knn_ms, 3), "P": P},
     }
