@@ -10,7 +10,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PMC = os.path.join(ROOT, "gpurun_out", "pmc")
 STAGE_OF = {"k_render_bwd": "render_bwd", "k_render_fwd": "render_fwd", "k_gaussian_backward": "gaussian_bwd",
             "k_preprocess": "preprocess", "k_duplicate": "duplicate", "k_finalize": "ranges",
-            "k_radix_scatter": "radix_scatter", "k_radix_upsweep": "radix_upsweep"}
+            "k_radix_scatter": "radix_scatter", "k_radix_upsweep": "radix_upsweep", "k_adam": "adam_step",
+            "k_activation_backward": "activation_backward"}
 
 
 def short(name):
