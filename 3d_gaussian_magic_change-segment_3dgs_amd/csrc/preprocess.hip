@@ -208,30 +208,35 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     // clear the depth sort's and the scan's look-back counters (saves two memset launches)
     zero16(zero_a, zero_a16, idx, (size_t)gridDim.x * blockDim.x);
     zero16(zero_b, zero_b16, idx, (size_t)gridDim.x * blockDim.x);
-    if (idx >= s.P) return;
+    // No early exits: the SH rows are staged through LDS by the whole block below, so
+    // every thread reaches the barriers; `ok` carries the reference's culls.
+    const bool live = idx < s.P;
+    const int sidx = live ? idx : 0;
     Cam cam;
     load_cam(s, cam);
-    radii[idx] = 0;
-    tiles_touched[idx] = 0;
-    depth_keys[idx] = 0xFFFFFFFFu;  // culled Gaussians sort last; they emit no instances
-    clamped[idx] = 0;
+    if (live) {
+        radii[idx] = 0;
+        tiles_touched[idx] = 0;
+        depth_keys[idx] = 0xFFFFFFFFu;  // culled Gaussians sort last; they emit no instances
+        clamped[idx] = 0;
+    }
 
-    const f3 p_orig = ld3(in.means3D + 3 * (size_t)idx);
+    const f3 p_orig = ld3(in.means3D + 3 * (size_t)sidx);
     // in_frustum (auxiliary.h:139-164)
     const f3 p_view = xform4x3(p_orig, cam.view);
-    if (p_view.z <= 0.2f) return;
+    bool ok = live && p_view.z > 0.2f;
     const float4 p_hom = xform4x4(p_orig, cam.proj);
     const float p_w = 1.0f / (p_hom.w + 0.0000001f);
     const f3 p_proj = {p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w};
 
     float c3[6];
     if (in.cov3D_precomp) {
-        const float* c = in.cov3D_precomp + 6 * (size_t)idx;
+        const float* c = in.cov3D_precomp + 6 * (size_t)sidx;
 #pragma unroll
         for (int i = 0; i < 6; ++i) c3[i] = c[i];
     } else {
-        const float4 q = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)idx);
-        cov3d_from(ld3(in.scales + 3 * (size_t)idx), s.scale_modifier, q, c3);
+        const float4 q = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)sidx);
+        cov3d_from(ld3(in.scales + 3 * (size_t)sidx), s.scale_modifier, q, c3);
     }
     const float focal_y = s.H / (2.0f * s.tanfovy);
     const float focal_x = s.W / (2.0f * s.tanfovx);
@@ -240,7 +245,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     const float cx = cov.m[0][0] + 0.3f, cy = cov.m[0][1], cz = cov.m[1][1] + 0.3f;
 
     const float det = (cx * cz - cy * cy);
-    if (det == 0.0f) return;
+    ok = ok && det != 0.0f;
     const float det_inv = 1.f / det;
     const float conic_x = cz * det_inv, conic_y = -cy * det_inv, conic_z = cx * det_inv;
     const float mid = 0.5f * (cx + cz);
@@ -248,23 +253,52 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     const float lambda2 = mid - sqrtf(fmaxf(0.1f, mid * mid - det));
     const float my_radius = ceilf(3.f * sqrtf(fmaxf(lambda1, lambda2)));
     const float px = ndc2pix(p_proj.x, s.W), py = ndc2pix(p_proj.y, s.H);
-    int x0, y0, x1, y1;
-    get_rect(px, py, (int)my_radius, gx, gy, x0, y0, x1, y1);
+    int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    if (ok) get_rect(px, py, (int)my_radius, gx, gy, x0, y0, x1, y1);
     const uint32_t ntiles = (uint32_t)((x1 - x0) * (y1 - y0));
-    if (ntiles == 0) return;
+    ok = ok && ntiles != 0;
 
-    f3 rgb;
+    f3 rgb = {0.f, 0.f, 0.f};
     uint8_t cbits = 0;
     if (in.colors_precomp == nullptr) {
         f3 dir = p_orig - cam.campos;
         dir = dir / sqrtf(dot3(dir, dir));
-        // per-coefficient loads: here they overlap the projection math better than a
-        // row of float4 loads issued up front (measured: 0.091 vs 0.100 ms at 1M)
-        const float* sh = in.shs + (size_t)idx * s.M * 3;
-        rgb = color_from_sh(s.D, dir, [&](int i) { return ld3(sh + 3 * i); }, cbits);
-    } else {
+        if (s.M == 16 && (reinterpret_cast<uintptr_t>(in.shs) & 15) == 0) {
+            // SH3 rows (192 B) through LDS: the wave loads 32 rows at a time as
+            // consecutive float4s (a thread loading its own row issues loads 192 B
+            // apart: 0.056 ms of a 0.100 ms kernel at 1M), then the 32 owners evaluate
+            // their colour from LDS.  Rows padded to 52 floats (2-way bank aliasing).
+            __shared__ float shrow[4][32][52];
+            const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+            const int wbase = blockIdx.x * blockDim.x + wave * 64;
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int g0 = wbase + 32 * h;
+                const float4* src = reinterpret_cast<const float4*>(in.shs + (size_t)g0 * 48);
+#pragma unroll
+                for (int r = 0; r < 6; ++r) {
+                    const int f = lane + 64 * r;  // float4 index in the 32-row run
+                    const int row = f / 12, col = f - 12 * (f / 12);
+                    if (g0 + row < s.P) *reinterpret_cast<float4*>(&shrow[wave][row][4 * col]) = src[f];
+                }
+                __syncthreads();
+                if ((lane >> 5) == h && ok) {
+                    const float* S = shrow[wave][lane & 31];
+                    rgb = color_from_sh(s.D, dir, [&](int i) { return f3{S[3 * i], S[3 * i + 1], S[3 * i + 2]}; },
+                                        cbits);
+                }
+                __syncthreads();
+            }
+        } else if (ok) {
+            // per-coefficient loads: here they overlap the projection math better than a
+            // row of float4 loads issued up front (measured: 0.091 vs 0.100 ms at 1M)
+            const float* sh = in.shs + (size_t)idx * s.M * 3;
+            rgb = color_from_sh(s.D, dir, [&](int i) { return ld3(sh + 3 * i); }, cbits);
+        }
+    } else if (ok) {
         rgb = ld3(in.colors_precomp + 3 * (size_t)idx);
     }
+    if (!ok) return;
     float s0 = 0.f, s1 = 0.f;
     if (in.segments) {
         const float2 sg = *reinterpret_cast<const float2*>(in.segments + 2 * (size_t)idx);
