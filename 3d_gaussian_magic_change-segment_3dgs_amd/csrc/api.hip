@@ -365,6 +365,91 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
     return 0;
 }
 
+size_t gsr_multiview_scratch_bytes(int P, int B) {
+    return gsr::align_up((size_t)(P > 0 ? P : 0) * (size_t)(B > 0 ? B : 0) * 16) + gsr::ALIGN;
+}
+
+int gsr_backward_multiview(int B, const gsr_view_state* views, const gsr_inputs* in, void* mv_scratch,
+                           const gsr_grads* grads, void* stream) {
+    using namespace gsr;
+    g_last_error.clear();
+    if (B < 1 || B > GSR_MAX_VIEWS) return fail("[gsr] multiview: B must be 1..16");
+    if (!views || !in || !grads) return fail("[gsr] multiview: null argument");
+    const gsr_settings* s0 = views[0].s;
+    if (!s0) return fail("[gsr] multiview: view 0 has no settings");
+    for (int v = 0; v < B; ++v) {
+        const gsr_view_state& V = views[v];
+        if (!V.s) return fail("[gsr] multiview: a view has no settings");
+        if (int rc = validate(V.s, in, false)) return rc;
+        if (V.s->P != s0->P || V.s->D != s0->D || V.s->M != s0->M || V.s->scale_modifier != s0->scale_modifier)
+            return fail("[gsr] multiview: P, D, M and scale_modifier must be equal across views");
+    }
+    const int P = s0->P;
+    if (P == 0) return 0;
+    if (in->shs && !mv_scratch) return fail("[gsr] multiview: scratch is NULL");
+    hipStream_t st = (hipStream_t)stream;
+    const bool dbg = s0->debug != 0;
+    MvArgs a{};
+    a.B = B;
+    for (int v = 0; v < B; ++v) {
+        const gsr_view_state& V = views[v];
+        const gsr_settings* s = V.s;
+        if (!V.geom || !V.img || !V.radii || !V.alpha || !V.dL_dcolor || !V.dL_dsegment || !V.dL_ddepth ||
+            !V.dL_dalpha)
+            return fail("[gsr] multiview: null buffer");
+        const size_t I = V.num_rendered > 0 ? (size_t)V.num_rendered : 0;
+        const ImgLayout IL = img_layout(s->W, s->H);
+        char* im = aligned_base(V.img);
+        const GeomLayout GL = geom_layout(P);
+        char* g = aligned_base(V.geom);
+        float* contrib = nullptr;
+        uint32_t* written = nullptr;
+        if (I > 0) {
+            if (!V.binning || !V.scratch) return fail("[gsr] multiview: binning/scratch buffer is NULL");
+            const BinLayout BL = bin_layout(I);
+            char* b = aligned_base(V.binning);
+            contrib = reinterpret_cast<float*>(aligned_base(V.scratch));
+            written = at<uint32_t>(b, BL.written);
+            {
+                StageScope sc(GSR_STAGE_RENDER_BWD, st);
+                launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order),
+                                       at<uint2>(im, IL.ranges), at<uint32_t>(b, BL.point_list),
+                                       at<uint32_t>(b, BL.slot_vals), at<float4>(g, GL.rec), s->bg, V.alpha,
+                                       at<uint32_t>(im, IL.n_contrib), V.dL_dcolor, V.dL_dsegment, V.dL_ddepth,
+                                       V.dL_dalpha, contrib, written, st);
+            }
+            GSR_STAGE("render backward");
+        } else {
+            // nothing rendered: every radius is 0 and the records are never read
+            written = nullptr;
+        }
+        MvView& w = a.v[v];
+        w.radii = V.radii;
+        w.tiles_touched = at<uint32_t>(g, GL.tiles_touched);
+        w.goff = at<uint32_t>(g, GL.goff);
+        w.clamped = at<uint8_t>(g, GL.clamped);
+        w.contrib = contrib;
+        w.written = written;
+        w.rec = at<float4>(g, GL.rec);
+        w.view = s->viewmatrix;
+        w.proj = s->projmatrix;
+        w.campos = s->campos;
+        w.dmeans2D = V.dmeans2D;
+        w.W = s->W;
+        w.H = s->H;
+        w.tanfovx = s->tanfovx;
+        w.tanfovy = s->tanfovy;
+    }
+    {
+        StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);
+        launch_gaussian_backward_multiview(P, s0->D, s0->M, s0->scale_modifier, *in, a, *grads,
+                                           reinterpret_cast<float4*>(in->shs ? aligned_base(mv_scratch) : nullptr),
+                                           st);
+    }
+    GSR_STAGE("gaussian backward (multiview)");
+    return 0;
+}
+
 int gsr_num_stages(void) { return NUM_STAGES; }
 
 const char* gsr_stage_name(int stage) { return (stage >= 0 && stage < NUM_STAGES) ? STAGE_NAMES[stage] : ""; }

@@ -166,6 +166,28 @@ void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int 
                        ushort4* rect, void* zero_a, size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes,
                        hipStream_t st);
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
+// Per-view inputs of the multi-view per-Gaussian backward (preprocess.hip).
+struct MvView {
+    const int* radii;
+    const uint32_t* tiles_touched;
+    const uint32_t* goff;
+    const uint8_t* clamped;
+    const float* contrib;
+    const uint32_t* written;
+    const float4* rec;
+    const float* view;
+    const float* proj;
+    const float* campos;
+    float* dmeans2D;
+    int W, H;
+    float tanfovx, tanfovy;
+};
+struct MvArgs {
+    int B;
+    MvView v[GSR_MAX_VIEWS];
+};
+void launch_gaussian_backward_multiview(int P, int D, int M, float scale_modifier, const gsr_inputs& in,
+                                        const MvArgs& a, const gsr_grads& g, float4* drgb, hipStream_t st);
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
                               const float* contrib, const uint32_t* written, const float4* rec,

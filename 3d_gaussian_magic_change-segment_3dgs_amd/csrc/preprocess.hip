@@ -665,6 +665,349 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
     }
 }
 
+
+// ------------------------------------------------------- multi-view backward --
+// Parameter gradients of B views summed (gsr_backward_multiview).  Two kernels:
+//  k_gaussian_backward_mv: per Gaussian, loops over the views: record gather,
+//    computeCov2DCUDA + preprocessCUDA backward per view (the view's camera), sums
+//    dmean / dcov3D / dopacity / dsegments / dcolors over the views, writes each
+//    view's dmeans2D, derives dscales / drot ONCE from the summed dcov3D (linear),
+//    and leaves each view's clamped dRGB for the SH kernel;
+//  k_gaussian_backward_mv_sh: per Gaussian, its SH row staged once through LDS
+//    (64 rows per wave, coalesced), loops over the views for the SH direction
+//    gradient and the dsh basis products, stores dsh once and adds the direction
+//    term into dmeans3D.
+// The shared inputs are read and the parameter gradients written once per batch.
+__global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, float scale_modifier, gsr_inputs in,
+                                                              MvArgs a, gsr_grads g, float4* __restrict__ drgb) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= P) return;
+    const size_t i3 = 3 * (size_t)idx;
+    const f3 mean = ld3(in.means3D + i3);
+    float c3[6];
+    float4 quat = make_float4(0.f, 0.f, 0.f, 0.f);
+    f3 scale = {0.f, 0.f, 0.f};
+    if (in.cov3D_precomp) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c3[i] = in.cov3D_precomp[6 * (size_t)idx + i];
+    } else {
+        quat = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)idx);
+        scale = ld3(in.scales + i3);
+        cov3d_from(scale, scale_modifier, quat, c3);
+    }
+    const M3 Vrk = vrk_of(c3);
+    const auto& V = Vrk.m;
+    f3 dmean_sum = {0.f, 0.f, 0.f}, dcol = {0.f, 0.f, 0.f};
+    float dcv_sum[6] = {0, 0, 0, 0, 0, 0};
+    float dop = 0.f, dseg0 = 0.f, dseg1 = 0.f;
+    for (int v = 0; v < a.B; ++v) {  // uniform: the view's fields are scalar loads
+        const MvView& w = a.v[v];
+        float4* drgb_v = drgb ? drgb + (size_t)v * P : nullptr;
+        if (!(w.radii[idx] > 0)) {
+            if (w.dmeans2D) { w.dmeans2D[i3] = 0.f; w.dmeans2D[i3 + 1] = 0.f; w.dmeans2D[i3 + 2] = 0.f; }
+            if (drgb_v) drgb_v[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+            continue;
+        }
+        const float4 r0 = w.rec[(size_t)idx * REC_F4], r1 = w.rec[(size_t)idx * REC_F4 + 1];
+        float q[12];
+#pragma unroll
+        for (int j = 0; j < 12; ++j) q[j] = 0.f;
+        {
+            const uint32_t lo = w.goff[idx], hi = lo + w.tiles_touched[idx];
+            for (uint32_t ww = lo >> 5; ww <= (hi - 1) >> 5; ++ww) {
+                uint32_t bits = w.written[ww];
+                if (ww == lo >> 5) bits &= ~0u << (lo & 31);
+                if (ww == (hi - 1) >> 5 && ((hi & 31) != 0)) bits &= ~(~0u << (hi & 31));
+                while (bits) {
+                    const uint32_t u = (ww << 5) + (uint32_t)__builtin_ctz(bits);
+                    bits &= bits - 1;
+                    const float4* src = reinterpret_cast<const float4*>(w.contrib + (size_t)u * 12);
+                    const float4 x = src[0], y = src[1], z = src[2];
+                    q[0] += x.x; q[1] += x.y; q[2] += x.z; q[3] += x.w;
+                    q[4] += y.x; q[5] += y.y; q[6] += y.z; q[7] += y.w;
+                    q[8] += z.x; q[9] += z.y; q[10] += z.z; q[11] += z.w;
+                }
+            }
+        }
+        const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
+        const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * w.W);
+        const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * w.H);
+        if (w.dmeans2D) { w.dmeans2D[i3] = dm2x; w.dmeans2D[i3 + 1] = dm2y; w.dmeans2D[i3 + 2] = 0.f; }
+        dcol = dcol + f3{q[0], q[1], q[2]};
+        dop += q[6];
+        dseg0 += q[3];
+        dseg1 += q[4];
+        if (drgb_v) {
+            const uint8_t cbits = w.clamped[idx];
+            drgb_v[idx] = make_float4((cbits & 1) ? 0.f : q[0], (cbits & 2) ? 0.f : q[1], (cbits & 4) ? 0.f : q[2],
+                                      0.f);
+        }
+        const float* view = w.view;
+        const float* proj = w.proj;
+        const float focal_y = w.H / (2.0f * w.tanfovy);
+        const float focal_x = w.W / (2.0f * w.tanfovx);
+        // ---- computeCov2DCUDA (backward.cu:155-273) for this view
+        const float dcx = -0.5f * op * q[9], dcy = -0.5f * op * q[10], dcz = -0.5f * op * q[11];
+        const EwaTerms e = ewa_terms(mean, focal_x, focal_y, w.tanfovx, w.tanfovy, view);
+        const float x_grad_mul = e.txtz < -e.limx || e.txtz > e.limx ? 0 : 1;
+        const float y_grad_mul = e.tytz < -e.limy || e.tytz > e.limy ? 0 : 1;
+        const M3& T = e.T;
+        const M3 cov2D = mmul(mmul(mtr(T), mtr(Vrk)), T);
+        const float a_ = cov2D.m[0][0] + 0.3f;
+        const float b_ = cov2D.m[0][1];
+        const float c_ = cov2D.m[1][1] + 0.3f;
+        const float denom = a_ * c_ - b_ * b_;
+        float dL_da = 0, dL_db = 0, dL_dc = 0;
+        const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+        const auto& Tt = T.m;
+        if (denom2inv != 0) {
+            dL_da = denom2inv * (-c_ * c_ * dcx + 2 * b_ * c_ * dcy + (denom - a_ * c_) * dcz);
+            dL_dc = denom2inv * (-a_ * a_ * dcz + 2 * a_ * b_ * dcy + (denom - a_ * c_) * dcx);
+            dL_db = denom2inv * 2 * (b_ * c_ * dcx - (denom + 2 * b_ * b_) * dcy + a_ * b_ * dcz);
+            dcv_sum[0] += (Tt[0][0] * Tt[0][0] * dL_da + Tt[0][0] * Tt[1][0] * dL_db + Tt[1][0] * Tt[1][0] * dL_dc);
+            dcv_sum[3] += (Tt[0][1] * Tt[0][1] * dL_da + Tt[0][1] * Tt[1][1] * dL_db + Tt[1][1] * Tt[1][1] * dL_dc);
+            dcv_sum[5] += (Tt[0][2] * Tt[0][2] * dL_da + Tt[0][2] * Tt[1][2] * dL_db + Tt[1][2] * Tt[1][2] * dL_dc);
+            dcv_sum[1] += 2 * Tt[0][0] * Tt[0][1] * dL_da + (Tt[0][0] * Tt[1][1] + Tt[0][1] * Tt[1][0]) * dL_db +
+                          2 * Tt[1][0] * Tt[1][1] * dL_dc;
+            dcv_sum[2] += 2 * Tt[0][0] * Tt[0][2] * dL_da + (Tt[0][0] * Tt[1][2] + Tt[0][2] * Tt[1][0]) * dL_db +
+                          2 * Tt[1][0] * Tt[1][2] * dL_dc;
+            dcv_sum[4] += 2 * Tt[0][2] * Tt[0][1] * dL_da + (Tt[0][1] * Tt[1][2] + Tt[0][2] * Tt[1][1]) * dL_db +
+                          2 * Tt[1][1] * Tt[1][2] * dL_dc;
+        }
+        const float dL_dT00 = 2 * (Tt[0][0] * V[0][0] + Tt[0][1] * V[0][1] + Tt[0][2] * V[0][2]) * dL_da +
+                              (Tt[1][0] * V[0][0] + Tt[1][1] * V[0][1] + Tt[1][2] * V[0][2]) * dL_db;
+        const float dL_dT01 = 2 * (Tt[0][0] * V[1][0] + Tt[0][1] * V[1][1] + Tt[0][2] * V[1][2]) * dL_da +
+                              (Tt[1][0] * V[1][0] + Tt[1][1] * V[1][1] + Tt[1][2] * V[1][2]) * dL_db;
+        const float dL_dT02 = 2 * (Tt[0][0] * V[2][0] + Tt[0][1] * V[2][1] + Tt[0][2] * V[2][2]) * dL_da +
+                              (Tt[1][0] * V[2][0] + Tt[1][1] * V[2][1] + Tt[1][2] * V[2][2]) * dL_db;
+        const float dL_dT10 = 2 * (Tt[1][0] * V[0][0] + Tt[1][1] * V[0][1] + Tt[1][2] * V[0][2]) * dL_dc +
+                              (Tt[0][0] * V[0][0] + Tt[0][1] * V[0][1] + Tt[0][2] * V[0][2]) * dL_db;
+        const float dL_dT11 = 2 * (Tt[1][0] * V[1][0] + Tt[1][1] * V[1][1] + Tt[1][2] * V[1][2]) * dL_dc +
+                              (Tt[0][0] * V[1][0] + Tt[0][1] * V[1][1] + Tt[0][2] * V[1][2]) * dL_db;
+        const float dL_dT12 = 2 * (Tt[1][0] * V[2][0] + Tt[1][1] * V[2][1] + Tt[1][2] * V[2][2]) * dL_dc +
+                              (Tt[0][0] * V[2][0] + Tt[0][1] * V[2][1] + Tt[0][2] * V[2][2]) * dL_db;
+        const auto& Wt = e.W.m;
+        const float dL_dJ00 = Wt[0][0] * dL_dT00 + Wt[0][1] * dL_dT01 + Wt[0][2] * dL_dT02;
+        const float dL_dJ02 = Wt[2][0] * dL_dT00 + Wt[2][1] * dL_dT01 + Wt[2][2] * dL_dT02;
+        const float dL_dJ11 = Wt[1][0] * dL_dT10 + Wt[1][1] * dL_dT11 + Wt[1][2] * dL_dT12;
+        const float dL_dJ12 = Wt[2][0] * dL_dT10 + Wt[2][1] * dL_dT11 + Wt[2][2] * dL_dT12;
+        const float hx = focal_x, hy = focal_y;
+        const f3 t = e.t;
+        const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+        const float dL_dtx = x_grad_mul * -hx * tz2 * dL_dJ02;
+        const float dL_dty = y_grad_mul * -hy * tz2 * dL_dJ12;
+        const float dL_dtz = -hx * tz2 * dL_dJ00 - hy * tz2 * dL_dJ11 + (2 * hx * t.x) * tz3 * dL_dJ02 +
+                             (2 * hy * t.y) * tz3 * dL_dJ12;
+        f3 dmean = xformVecT({dL_dtx, dL_dty, dL_dtz}, view);
+        // ---- preprocessCUDA backward (backward.cu:372-403) for this view
+        const f3 m = mean;
+        const float4 m_hom = xform4x4(m, proj);
+        const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+        const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+        const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+        f3 dm;
+        dm.x = (proj[0] * m_w - proj[3] * mul1) * dm2x + (proj[1] * m_w - proj[3] * mul2) * dm2y;
+        dm.y = (proj[4] * m_w - proj[7] * mul1) * dm2x + (proj[5] * m_w - proj[7] * mul2) * dm2y;
+        dm.z = (proj[8] * m_w - proj[11] * mul1) * dm2x + (proj[9] * m_w - proj[11] * mul2) * dm2y;
+        dmean = dmean + dm;
+        const float ddepth = q[5];
+        const float mul3 = view[2] * m.x + view[6] * m.y + view[10] * m.z + view[14];
+        f3 dmz;
+        dmz.x = (view[2] - view[3] * mul3) * ddepth;
+        dmz.y = (view[6] - view[7] * mul3) * ddepth;
+        dmz.z = (view[10] - view[11] * mul3) * ddepth;
+        dmean = dmean + dmz;
+        dmean_sum = dmean_sum + dmean;
+    }
+    if (g.dcolors) { g.dcolors[i3] = dcol.x; g.dcolors[i3 + 1] = dcol.y; g.dcolors[i3 + 2] = dcol.z; }
+    if (g.dopacity) g.dopacity[idx] = dop;
+    if (g.dsegments) { g.dsegments[2 * (size_t)idx] = dseg0; g.dsegments[2 * (size_t)idx + 1] = dseg1; }
+    if (g.dcov3D)
+#pragma unroll
+        for (int i = 0; i < 6; ++i) g.dcov3D[6 * (size_t)idx + i] = dcv_sum[i];
+    // dmeans3D without the SH direction term (k_gaussian_backward_mv_sh adds it)
+    if (g.dmeans3D) { g.dmeans3D[i3] = dmean_sum.x; g.dmeans3D[i3 + 1] = dmean_sum.y; g.dmeans3D[i3 + 2] = dmean_sum.z; }
+    if (in.scales) {
+        // computeCov3D backward (backward.cu:276-341) of the summed dcov3D (linear in it)
+        const float* dcv = dcv_sum;
+        const float r = quat.x, x = quat.y, y = quat.z, z = quat.w;
+        const M3 R = mat3(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                          2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                          2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+        M3 S = mat3(1, 0, 0, 0, 1, 0, 0, 0, 1);
+        const f3 sv = scale_modifier * scale;
+        S.m[0][0] = sv.x;
+        S.m[1][1] = sv.y;
+        S.m[2][2] = sv.z;
+        const M3 Mm = mmul(S, R);
+        const M3 dSig = mat3(dcv[0], 0.5f * dcv[1], 0.5f * dcv[2], 0.5f * dcv[1], dcv[3], 0.5f * dcv[4],
+                             0.5f * dcv[2], 0.5f * dcv[4], dcv[5]);
+        M3 M2;
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc)
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) M2.m[cc][rr] = 2.0f * Mm.m[cc][rr];
+        const M3 dM = mmul(M2, dSig);
+        const M3 Rt = mtr(R);
+        M3 dMt = mtr(dM);
+        if (g.dscales) {
+            g.dscales[i3 + 0] = Rt.m[0][0] * dMt.m[0][0] + Rt.m[0][1] * dMt.m[0][1] + Rt.m[0][2] * dMt.m[0][2];
+            g.dscales[i3 + 1] = Rt.m[1][0] * dMt.m[1][0] + Rt.m[1][1] * dMt.m[1][1] + Rt.m[1][2] * dMt.m[1][2];
+            g.dscales[i3 + 2] = Rt.m[2][0] * dMt.m[2][0] + Rt.m[2][1] * dMt.m[2][1] + Rt.m[2][2] * dMt.m[2][2];
+        }
+#pragma unroll
+        for (int rr = 0; rr < 3; ++rr) {
+            dMt.m[0][rr] *= sv.x;
+            dMt.m[1][rr] *= sv.y;
+            dMt.m[2][rr] *= sv.z;
+        }
+        const auto& d = dMt.m;
+        if (g.drot) {
+            float* dr = g.drot + 4 * (size_t)idx;
+            dr[0] = 2 * z * (d[0][1] - d[1][0]) + 2 * y * (d[2][0] - d[0][2]) + 2 * x * (d[1][2] - d[2][1]);
+            dr[1] = 2 * y * (d[1][0] + d[0][1]) + 2 * z * (d[2][0] + d[0][2]) + 2 * r * (d[1][2] - d[2][1]) -
+                    4 * x * (d[2][2] + d[1][1]);
+            dr[2] = 2 * x * (d[1][0] + d[0][1]) + 2 * r * (d[2][0] - d[0][2]) + 2 * z * (d[1][2] + d[2][1]) -
+                    4 * y * (d[2][2] + d[0][0]);
+            dr[3] = 2 * r * (d[0][1] - d[1][0]) + 2 * x * (d[2][0] + d[0][2]) + 2 * y * (d[1][2] + d[2][1]) -
+                    4 * z * (d[1][1] + d[0][0]);
+        }
+    }
+}
+
+// SH part of the multi-view backward.  STAGED: M == 16 with 16-B aligned rows, the
+// wave's 64 rows go through LDS both ways (coalesced 12 KB runs); otherwise rows are
+// read / written per thread.
+template <bool STAGED>
+__global__ void __launch_bounds__(256) k_gaussian_backward_mv_sh(int P, int D, int M, const float* __restrict__ shs,
+                                                                 const float* __restrict__ means3D, MvArgs a,
+                                                                 const float4* __restrict__ drgb,
+                                                                 float* __restrict__ dsh,
+                                                                 float* __restrict__ dmeans3D) {
+    __shared__ float rows[STAGED ? 4 : 1][STAGED ? 64 : 1][52];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wbase = blockIdx.x * blockDim.x + wave * 64;
+    const int idx = wbase + lane;
+    const bool live = idx < P;
+    if (STAGED) {
+        const float4* src = reinterpret_cast<const float4*>(shs + (size_t)wbase * 48);
+#pragma unroll
+        for (int r = 0; r < 12; ++r) {
+            const int f = lane + 64 * r;  // float4 index in the wave's 64-row run
+            const int row = f / 12, col = f - 12 * (f / 12);
+            if (wbase + row < P) *reinterpret_cast<float4*>(&rows[wave][row][4 * col]) = src[f];
+        }
+        __syncthreads();
+    } else if (!live) {
+        return;
+    }
+    ShRow Sreg;
+    if (!STAGED && live) Sreg.load(shs + (size_t)idx * M * 3, M, (D + 1) * (D + 1));
+    const float* Sl = rows[STAGED ? wave : 0][STAGED ? lane : 0];
+    auto S = [&](int i) -> f3 {
+        if (STAGED) return f3{Sl[3 * i], Sl[3 * i + 1], Sl[3 * i + 2]};
+        return Sreg(i);
+    };
+    float acc[48];
+#pragma unroll
+    for (int i = 0; i < 48; ++i) acc[i] = 0.f;
+    f3 dn_sum = {0.f, 0.f, 0.f};
+    const f3 mean = live ? ld3(means3D + 3 * (size_t)idx) : f3{0.f, 0.f, 0.f};
+    for (int v = 0; v < a.B; ++v) {
+        const float4 c = live ? drgb[(size_t)v * P + idx] : make_float4(0.f, 0.f, 0.f, 0.f);
+        if (c.x == 0.f && c.y == 0.f && c.z == 0.f) continue;  // invisible in this view (or a zero gradient)
+        const f3 dRGB = {c.x, c.y, c.z};
+        const f3 dir_orig = mean - ld3(a.v[v].campos);
+        const f3 dir = dir_orig / sqrtf(dot3(dir_orig, dir_orig));
+        float bas[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) bas[i] = 0.f;
+        f3 dx = {0, 0, 0}, dy = {0, 0, 0}, dz = {0, 0, 0};
+        const float x = dir.x, y = dir.y, z = dir.z;
+        bas[0] = C_SH0;
+        if (D > 0) {
+            bas[1] = -C_SH1 * y; bas[2] = C_SH1 * z; bas[3] = -C_SH1 * x;
+            dx = -C_SH1 * S(3);
+            dy = -C_SH1 * S(1);
+            dz = C_SH1 * S(2);
+            if (D > 1) {
+                const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                bas[4] = C_SH2[0] * xy;
+                bas[5] = C_SH2[1] * yz;
+                bas[6] = C_SH2[2] * (2.f * zz - xx - yy);
+                bas[7] = C_SH2[3] * xz;
+                bas[8] = C_SH2[4] * (xx - yy);
+                dx = dx + (C_SH2[0] * y * S(4) + C_SH2[2] * 2.f * -x * S(6) + C_SH2[3] * z * S(7) +
+                           C_SH2[4] * 2.f * x * S(8));
+                dy = dy + (C_SH2[0] * x * S(4) + C_SH2[1] * z * S(5) + C_SH2[2] * 2.f * -y * S(6) +
+                           C_SH2[4] * 2.f * -y * S(8));
+                dz = dz + (C_SH2[1] * y * S(5) + C_SH2[2] * 2.f * 2.f * z * S(6) + C_SH2[3] * x * S(7));
+                if (D > 2) {
+                    bas[9] = C_SH3[0] * y * (3.f * xx - yy);
+                    bas[10] = C_SH3[1] * xy * z;
+                    bas[11] = C_SH3[2] * y * (4.f * zz - xx - yy);
+                    bas[12] = C_SH3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                    bas[13] = C_SH3[4] * x * (4.f * zz - xx - yy);
+                    bas[14] = C_SH3[5] * z * (xx - yy);
+                    bas[15] = C_SH3[6] * x * (xx - 3.f * yy);
+                    dx = dx + (C_SH3[0] * S(9) * 3.f * 2.f * xy + C_SH3[1] * S(10) * yz +
+                               C_SH3[2] * S(11) * -2.f * xy + C_SH3[3] * S(12) * -3.f * 2.f * xz +
+                               C_SH3[4] * S(13) * (-3.f * xx + 4.f * zz - yy) + C_SH3[5] * S(14) * 2.f * xz +
+                               C_SH3[6] * S(15) * 3.f * (xx - yy));
+                    dy = dy + (C_SH3[0] * S(9) * 3.f * (xx - yy) + C_SH3[1] * S(10) * xz +
+                               C_SH3[2] * S(11) * (-3.f * yy + 4.f * zz - xx) + C_SH3[3] * S(12) * -3.f * 2.f * yz +
+                               C_SH3[4] * S(13) * -2.f * xy + C_SH3[5] * S(14) * -2.f * yz +
+                               C_SH3[6] * S(15) * -3.f * 2.f * xy);
+                    dz = dz + (C_SH3[1] * S(10) * xy + C_SH3[2] * S(11) * 4.f * 2.f * yz +
+                               C_SH3[3] * S(12) * 3.f * (2.f * zz - xx - yy) + C_SH3[4] * S(13) * 4.f * 2.f * xz +
+                               C_SH3[5] * S(14) * (xx - yy));
+                }
+            }
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            acc[3 * i] += bas[i] * dRGB.x;
+            acc[3 * i + 1] += bas[i] * dRGB.y;
+            acc[3 * i + 2] += bas[i] * dRGB.z;
+        }
+        const f3 dv = {dot3(dx, dRGB), dot3(dy, dRGB), dot3(dz, dRGB)};
+        // dnormvdv (auxiliary.h:107-117)
+        const f3 vv = dir_orig;
+        const float sum2 = vv.x * vv.x + vv.y * vv.y + vv.z * vv.z;
+        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+        f3 dn;
+        dn.x = ((+sum2 - vv.x * vv.x) * dv.x - vv.y * vv.x * dv.y - vv.z * vv.x * dv.z) * invsum32;
+        dn.y = (-vv.x * vv.y * dv.x + (sum2 - vv.y * vv.y) * dv.y - vv.z * vv.y * dv.z) * invsum32;
+        dn.z = (-vv.x * vv.z * dv.x - vv.y * vv.z * dv.y + (sum2 - vv.z * vv.z) * dv.z) * invsum32;
+        dn_sum = dn_sum + dn;
+    }
+    if (live && dmeans3D) {
+        float* o = dmeans3D + 3 * (size_t)idx;
+        o[0] += dn_sum.x;
+        o[1] += dn_sum.y;
+        o[2] += dn_sum.z;
+    }
+    if (!dsh) return;  // uniform
+    if (STAGED) {
+        __syncthreads();  // every lane has read its SH row
+        float* row = rows[wave][lane];
+#pragma unroll
+        for (int i = 0; i < 12; ++i)
+            *reinterpret_cast<float4*>(row + 4 * i) = make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2],
+                                                                  acc[4 * i + 3]);
+        __syncthreads();
+        float4* dst = reinterpret_cast<float4*>(dsh + (size_t)wbase * 48);
+#pragma unroll
+        for (int r = 0; r < 12; ++r) {
+            const int f = lane + 64 * r;
+            const int rr = f / 12, col = f - 12 * (f / 12);
+            if (wbase + rr < P) dst[f] = *reinterpret_cast<const float4*>(&rows[wave][rr][4 * col]);
+        }
+    } else {
+        float* o = dsh + (size_t)idx * M * 3;
+        for (int f = 0; f < 3 * M; ++f) o[f] = f < 48 ? acc[f] : 0.f;
+    }
+}
 }  // namespace
 
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec, int* radii,
@@ -679,6 +1022,23 @@ void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
     if (P == 0) return;
     hipLaunchKernelGGL(k_mark_visible, dim3(cdiv(P, 256)), dim3(256), 0, st, P, means3D, view, present);
+}
+
+void launch_gaussian_backward_multiview(int P, int D, int M, float scale_modifier, const gsr_inputs& in,
+                                        const MvArgs& a, const gsr_grads& g, float4* drgb, hipStream_t st) {
+    if (P == 0) return;
+    float4* drgb_used = (in.shs && (g.dsh || g.dmeans3D)) ? drgb : nullptr;
+    hipLaunchKernelGGL(k_gaussian_backward_mv, dim3(cdiv(P, 256)), dim3(256), 0, st, P, M, scale_modifier, in, a, g,
+                       drgb_used);
+    if (!drgb_used) return;
+    const bool staged = M == 16 && (reinterpret_cast<uintptr_t>(in.shs) & 15) == 0 &&
+                        (!g.dsh || (reinterpret_cast<uintptr_t>(g.dsh) & 15) == 0);
+    if (staged)
+        hipLaunchKernelGGL(k_gaussian_backward_mv_sh<true>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, in.shs,
+                           in.means3D, a, drgb_used, g.dsh, g.dmeans3D);
+    else
+        hipLaunchKernelGGL(k_gaussian_backward_mv_sh<false>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, in.shs,
+                           in.means3D, a, drgb_used, g.dsh, g.dmeans3D);
 }
 
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,

@@ -71,6 +71,21 @@ _lib.gsr_version.restype = ctypes.c_char_p
 _lib.gsr_debug_copy.restype = ctypes.c_longlong
 _lib.gsr_debug_copy.argtypes = [ctypes.c_char_p, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]
 
+class _ViewState(ctypes.Structure):
+    _fields_ = [("s", ctypes.POINTER(_Settings)), ("radii", ctypes.c_void_p), ("geom", ctypes.c_void_p),
+                ("binning", ctypes.c_void_p), ("img", ctypes.c_void_p), ("num_rendered", ctypes.c_int),
+                ("alpha", ctypes.c_void_p), ("dL_dcolor", ctypes.c_void_p), ("dL_dsegment", ctypes.c_void_p),
+                ("dL_ddepth", ctypes.c_void_p), ("dL_dalpha", ctypes.c_void_p), ("scratch", ctypes.c_void_p),
+                ("dmeans2D", ctypes.c_void_p)]
+
+
+MAX_VIEWS = 16  # include/gsr.h GSR_MAX_VIEWS
+_lib.gsr_multiview_scratch_bytes.restype = _sz
+_lib.gsr_multiview_scratch_bytes.argtypes = [_i, _i]
+_lib.gsr_backward_multiview.restype = _i
+_lib.gsr_backward_multiview.argtypes = [_i, ctypes.POINTER(_ViewState), ctypes.POINTER(_Inputs), _vp,
+                                        ctypes.POINTER(_Grads), _vp]
+
 _ll = ctypes.c_longlong
 _lib.gsr_arena_layout.restype = _ll
 _lib.gsr_arena_layout.argtypes = [_i, _i, _i, ctypes.POINTER(_ll)]
@@ -88,7 +103,8 @@ _lib.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POIN
 EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_img_bytes", "gsr_backward_scratch_bytes",
                     "gsr_forward_geometry", "gsr_forward_render", "gsr_backward", "gsr_mark_visible",
                     "gsr_debug_copy", "gsr_num_stages", "gsr_stage_name", "gsr_timing_enable", "gsr_timing_collect",
-                    "gsr_last_error", "gsr_version", "gsr_set_option")
+                    "gsr_last_error", "gsr_version", "gsr_set_option", "gsr_multiview_scratch_bytes",
+                    "gsr_backward_multiview")
 
 _DEBUG_FIELDS = {  # name -> (dtype, elements per unit, unit: P | I | T)
     "tiles_touched": (torch.int32, 1, "P"), "rec": (torch.float32, 16, "P"), "clamped": (torch.uint8, 1, "P"),
@@ -350,3 +366,87 @@ def mark_visible(means3D, viewmatrix, projmatrix):
         _check(_lib.gsr_mark_visible(P, m.data_ptr(), v.data_ptr(), p.data_ptr(), present.data_ptr(),
                                      _stream(device)))
     return present
+
+
+def rasterize_gaussians_backward_multiview(views, means3D, colors, segments, scales, rotations, scale_modifier,
+                                           cov3D_precomp, sh, degree, debug):
+    """gsr_backward_multiview: the summed parameter gradients of several views.
+    `views` holds, per view, the raster settings fields (bg, viewmatrix, projmatrix,
+    tanfovx, tanfovy, image_height, image_width, campos), the forward state
+    (radii, geom, binning, img, num_rendered, alpha) and the upstream gradients
+    (dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha; None = zeros).  Returns the
+    single-view tuple (dmeans2D = None, dcolors, dopacity, dmeans3D, dcov3D, dsh,
+    dscales, drot, dsegments) -- one gradient arena, bucket first -- and the list of
+    per-view dmeans2D [P,3]."""
+    B = len(views)
+    if not 1 <= B <= MAX_VIEWS:
+        raise RuntimeError(f"multiview backward: 1..{MAX_VIEWS} views per call")
+    P = int(means3D.size(0))
+    device = means3D.device
+    with torch.cuda.device(device):
+        means3D_ = _dev_f32(means3D, device, "means3D")
+        sh_ = _dev_f32(sh, device, "sh")
+        colors_ = _dev_f32(colors, device, "colors_precomp")
+        segments_ = _dev_f32(segments, device, "segments", align=8)
+        scales_ = _dev_f32(scales, device, "scales")
+        rotations_ = _dev_f32(rotations, device, "rotations", align=16)
+        cov_ = _dev_f32(cov3D_precomp, device, "cov3D_precomp")
+        M = int(sh_.size(1)) if sh_ is not None else 0
+        lay = grad_arena_layout(P, M)
+        arena = torch.empty(lay["total"][1], dtype=torch.float32, device=device)
+
+        def view_(name, *shape):
+            o, k = lay[name]
+            return arena.narrow(0, o, k * P).view(P, *shape)
+
+        dmeans3D, dsh, dopacity = view_("dmeans3D", 3), view_("dsh", M, 3), view_("dopacity", 1)
+        dscales, drot, dsegments = view_("dscales", 3), view_("drot", 4), view_("dsegments", NUM_CLASS)
+        dcolors, dcov3D = view_("dcolors", 3), view_("dcov3D", 6)
+        f32 = dict(dtype=torch.float32, device=device)
+        d2 = [torch.empty(P, 3, **f32) for _ in range(B)]
+        out = (None, dcolors if colors_ is not None else None, dopacity, dmeans3D,
+               dcov3D if cov_ is not None else None, dsh if sh_ is not None else None,
+               dscales if scales_ is not None else None, drot if scales_ is not None else None,
+               dsegments if segments_ is not None else None)
+        if P == 0:
+            arena.zero_()
+            return out, d2
+        keep = []  # ctypes structs and converted tensors must outlive the call
+        states = (_ViewState * B)()
+        for v, V in enumerate(views):
+            H, W = int(V["image_height"]), int(V["image_width"])
+            bg_ = _dev_f32(V["bg"], device, "bg")
+            vm = _dev_f32(V["viewmatrix"], device, "viewmatrix")
+            pm = _dev_f32(V["projmatrix"], device, "projmatrix")
+            cp = _dev_f32(V["campos"], device, "campos")
+            st = _settings(P, int(degree), M, W, H, V["tanfovx"], V["tanfovy"], scale_modifier, False, debug, bg_,
+                           vm, pm, cp)
+            ups = [_dev_f32(V[n], device, n) for n in ("dL_dcolor", "dL_dsegment", "dL_ddepth", "dL_dalpha")]
+            ups = [u if u is not None else torch.zeros(c, H, W, **f32)
+                   for u, c in zip(ups, (NUM_CHANNELS, NUM_CLASS, 1, 1))]
+            alpha_ = _dev_f32(V["alpha"], device, "alpha")
+            R = int(V["num_rendered"])
+            scratch = torch.empty(_lib.gsr_backward_scratch_bytes(R), dtype=torch.uint8, device=device)
+            radii_ = V["radii"].contiguous()
+            keep += [st, bg_, vm, pm, cp, ups, alpha_, scratch, radii_]
+            S = states[v]
+            S.s = ctypes.pointer(st)
+            S.radii, S.geom = radii_.data_ptr(), V["geom"].data_ptr()
+            S.binning = V["binning"].data_ptr() if V["binning"].numel() else None
+            S.img, S.num_rendered, S.alpha = V["img"].data_ptr(), R, alpha_.data_ptr()
+            S.dL_dcolor, S.dL_dsegment, S.dL_ddepth, S.dL_dalpha = (u.data_ptr() for u in ups)
+            S.scratch = scratch.data_ptr() if R > 0 else None
+            S.dmeans2D = d2[v].data_ptr()
+        inp = _inputs(means3D_, sh_, colors_, segments_, None, scales_, rotations_, cov_)
+        mv = torch.empty(_lib.gsr_multiview_scratch_bytes(P, B), dtype=torch.uint8, device=device)
+        g = _Grads()
+        g.dmeans2D, g.dopacity, g.dmeans3D = None, dopacity.data_ptr(), dmeans3D.data_ptr()
+        g.dcolors = dcolors.data_ptr() if colors_ is not None else None
+        g.dcov3D = dcov3D.data_ptr() if cov_ is not None else None
+        g.dsh = dsh.data_ptr() if (sh_ is not None and M > 0) else None
+        g.dscales = dscales.data_ptr() if scales_ is not None else None
+        g.drot = drot.data_ptr() if scales_ is not None else None
+        g.dsegments = dsegments.data_ptr()
+        _check(_lib.gsr_backward_multiview(B, states, ctypes.byref(inp), mv.data_ptr(), ctypes.byref(g),
+                                           _stream(device)))
+    return out, d2

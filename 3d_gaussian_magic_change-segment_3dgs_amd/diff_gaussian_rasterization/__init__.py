@@ -14,7 +14,8 @@ import torch.nn as nn
 
 from . import _C
 
-__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians"]
+__all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
+           "rasterize_gaussians_multiview"]
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -155,6 +156,65 @@ class _RasterizeGaussians(torch.autograd.Function):
             None,
         )
         return grads
+
+
+def rasterize_gaussians_multiview(means3D, means2D_list, sh, colors_precomp, segments, opacities, scales, rotations,
+                                  cov3Ds_precomp, raster_settings_list):
+    """Several views of the same Gaussians (the batch of a view-parallel trainer step):
+    per view the forward of rasterize_gaussians, and ONE backward that sums the
+    parameter gradients over the views (include/gsr.h gsr_backward_multiview; the
+    per-Gaussian work and parameter traffic happen once per batch).  means2D_list
+    holds one screen-space dummy per view (its .grad is that view's gradient, for
+    the densification statistics).  Returns a list of (color, radii, depth, alpha,
+    segment) per view.  Same inputs and conventions as rasterize_gaussians; an
+    extension of the reference API (which renders one view per call)."""
+    B = len(raster_settings_list)
+    if B != len(means2D_list):
+        raise ValueError("one means2D per view")
+    outs = _RasterizeGaussiansMultiview.apply(means3D, sh, colors_precomp, segments, opacities, scales, rotations,
+                                              cov3Ds_precomp, tuple(raster_settings_list), *means2D_list)
+    return [tuple(outs[5 * v:5 * v + 5]) for v in range(B)]
+
+
+class _RasterizeGaussiansMultiview(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, means3D, sh, colors_precomp, segments, opacities, scales, rotations, cov3Ds_precomp,
+                settings_list, *means2D_list):
+        outs, views = [], []
+        for rs in settings_list:
+            out = _C.rasterize_gaussians(rs.bg, means3D, colors_precomp, segments, opacities, scales, rotations,
+                                         rs.scale_modifier, cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx,
+                                         rs.tanfovy, rs.image_height, rs.image_width, sh, rs.sh_degree, rs.campos,
+                                         rs.prefiltered, rs.debug)
+            num_rendered, color, depth, segment, alpha, radii, geom, binning, img = out
+            views.append((num_rendered, radii, geom, binning, img, alpha))
+            ctx.mark_non_differentiable(radii)
+            outs += [color, radii, depth, alpha, segment]
+        ctx.settings_list = settings_list
+        ctx.views = views
+        ctx.save_for_backward(colors_precomp, segments, means3D, scales, rotations, cov3Ds_precomp, sh)
+        ctx.set_materialize_grads(False)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *grad_outputs):
+        colors_precomp, segments, means3D, scales, rotations, cov3Ds_precomp, sh = ctx.saved_tensors
+        rs0 = ctx.settings_list[0]
+        views = []
+        for v, (rs, st) in enumerate(zip(ctx.settings_list, ctx.views)):
+            num_rendered, radii, geom, binning, img, alpha = st
+            gc, _, gd, ga, gs = grad_outputs[5 * v:5 * v + 5]
+            views.append({"bg": rs.bg, "viewmatrix": rs.viewmatrix, "projmatrix": rs.projmatrix,
+                          "tanfovx": rs.tanfovx, "tanfovy": rs.tanfovy, "image_height": rs.image_height,
+                          "image_width": rs.image_width, "campos": rs.campos, "radii": radii, "geom": geom,
+                          "binning": binning, "img": img, "num_rendered": num_rendered, "alpha": alpha,
+                          "dL_dcolor": gc, "dL_dsegment": gs, "dL_ddepth": gd, "dL_dalpha": ga})
+        (_, g_colors, g_opacities, g_means3D, g_cov3D, g_sh, g_scales, g_rot, g_segments), d2 = \
+            _C.rasterize_gaussians_backward_multiview(views, means3D, colors_precomp, segments, scales, rotations,
+                                                      rs0.scale_modifier, cov3Ds_precomp, sh, rs0.sh_degree,
+                                                      rs0.debug)
+        ctx.views = None
+        return (g_means3D, g_sh, g_colors, g_segments, g_opacities, g_scales, g_rot, g_cov3D, None, *d2)
 
 
 class GaussianRasterizationSettings(NamedTuple):

@@ -1,13 +1,16 @@
 #!/usr/bin/env python
 """bench.py -- forward+backward views/s of the gsr rasterizer (BASELINE.json metric).
 
-One step = one view through the drop-in boundary: _RasterizeGaussians.forward
-(incl. the reference's num_rendered host sync) + .backward with fixed synthetic
-upstream gradients, on the synthetic metric scene (1M Gaussians,
-SH3, 2 segment classes, 1920x1080) resident in HBM.  With N GPUs (torchrun, one
-process per GPU) every rank renders its own view of the replicated scene and the
-parameter-gradient bucket (61 f32 / Gaussian) is summed with one RCCL all-reduce
-per step; value = N * steps / max-over-ranks elapsed (weak scaling in views).
+One step = the batch of a view-parallel trainer: every rank renders B views
+(--views-per-gpu, default 8) of the replicated synthetic metric scene (1M
+Gaussians, SH3, 2 segment classes, 1920x1080, resident in HBM) -- per view the
+forward at the boundary (incl. the reference's num_rendered host sync) -- then ONE
+backward of the B views with fixed synthetic upstream gradients
+that sums the parameter gradients over them (gsr_backward_multiview), and with N
+GPUs (torchrun, one process per GPU) one RCCL all-reduce of the parameter-gradient
+bucket (61 f32 / Gaussian) per step.  value = N * B * steps / max-over-ranks
+elapsed (weak scaling in views).  --views-per-gpu 1 times the drop-in single-view
+API alone; at N = 1 the default run also reports it as `drop_in_single_view`.
 
 Prints ONE JSON line on rank 0.  Extra objects:
   roofline     -- the dominant kernel (per-stage HIP events recorded by libgsr on
@@ -43,7 +46,7 @@ SIMD_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1_pmc_summary.json")
 
 
-def algorithmic_bytes(stage, P, I, HW, deg, launches_per_view=1):
+def algorithmic_bytes(stage, P, I, HW, deg, views=1):
     """Bytes a stage must move per launch: SURVEY.md s8(d)'s per-unit figures
     (a7..a16) attributed to the gsr stage that does that work."""
     M = (deg + 1) ** 2
@@ -63,8 +66,8 @@ def algorithmic_bytes(stage, P, I, HW, deg, launches_per_view=1):
         return 52 * I + 32 * HW
     if stage == "render_bwd":      # a14 (per-instance + per-pixel part)
         return 52 * I + 36 * HW
-    if stage == "gaussian_bwd":    # a14 grad outs + a15 + a16: 56 + 92 + (151 + 24 M) B per Gaussian
-        return (56 + 92 + 151 + 24 * M) * P
+    if stage == "gaussian_bwd":    # a14 grad outs + a15 + a16: 56 + 92 + (151 + 24 M) B per Gaussian and view
+        return (56 + 92 + 151 + 24 * M) * P * views
     return 0
 
 
@@ -104,6 +107,9 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work for cpu_baseline")
     ap.add_argument("--stages", action="store_true", help="print the per-stage table to stderr")
     ap.add_argument("--no-train", action="store_true", help="skip the train_step measurement (SURVEY.md s8f)")
+    ap.add_argument("--views-per-gpu", type=int, default=8,
+                    help="views per rank per step (1: the drop-in single-view API; >1: one multi-view backward "
+                         "and one gradient all-reduce per step)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -131,7 +137,11 @@ def main():
     import diff_gaussian_rasterization as dgr
     from diff_gaussian_rasterization import _C
 
-    scene_cpu, cam_cpu = config_scene_and_camera(args.config, view_index=rank, n_views=max(8, world))
+    B = max(1, min(args.views_per_gpu, 16))
+    n_views = max(8, world * B)
+    scene_cpu, cam_cpu = config_scene_and_camera(args.config, view_index=rank * B, n_views=n_views)
+    cams_cpu = [cam_cpu] + [config_scene_and_camera(args.config, view_index=rank * B + j, n_views=n_views, P=1)[1]
+                            for j in range(1, B)]
     P, W, H, deg = scene_cpu.P, cam_cpu.width, cam_cpu.height, scene_cpu.sh_degree
     gen = torch.Generator().manual_seed(1)
     ups_cpu = {k: (torch.randn(c, H, W, generator=gen) * 1e-3) for k, c in
@@ -140,23 +150,32 @@ def main():
     leaf = lambda t: t.to(device).contiguous().requires_grad_(True)
     means3D, shs, opac = leaf(scene_cpu.means3D), leaf(scene_cpu.shs), leaf(scene_cpu.opacities)
     scales, rots, segs = leaf(scene_cpu.scales), leaf(scene_cpu.rotations), leaf(scene_cpu.segments)
-    means2D = torch.zeros_like(means3D, requires_grad=True)
+    means2D = [torch.zeros_like(means3D, requires_grad=True) for _ in range(B)]
     E = torch.empty(0, device=device)
-    settings = dgr.GaussianRasterizationSettings(
-        image_height=H, image_width=W, tanfovx=cam_cpu.tanfovx, tanfovy=cam_cpu.tanfovy,
-        bg=torch.zeros(3, device=device), scale_modifier=1.0, viewmatrix=cam_cpu.world_view_transform.to(device),
-        projmatrix=cam_cpu.full_proj_transform.to(device), sh_degree=deg, campos=cam_cpu.camera_center.to(device),
-        prefiltered=False, debug=False)
-    inputs = [means3D, means2D, shs, opac, scales, rots, segs]
+    settings = [dgr.GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy,
+        bg=torch.zeros(3, device=device), scale_modifier=1.0, viewmatrix=c.world_view_transform.to(device),
+        projmatrix=c.full_proj_transform.to(device), sh_degree=deg, campos=c.camera_center.to(device),
+        prefiltered=False, debug=False) for c in cams_cpu]
+    params = [means3D, shs, opac, scales, rots, segs]
     lay = _C.grad_arena_layout(P, shs.shape[1])
     state = {"I": 0}
+    up_list = [ups["color"], ups["depth"], ups["alpha"], ups["segment"]]
 
     def step():
-        color, radii, depth, alpha, segment = dgr.rasterize_gaussians(means3D, means2D, shs, E, segs, opac, scales,
-                                                                      rots, E, settings)
-        state["I"] = color.grad_fn.num_rendered
-        g = torch.autograd.grad([color, depth, alpha, segment],
-                                inputs, [ups["color"], ups["depth"], ups["alpha"], ups["segment"]])
+        if B == 1:
+            # one view through the drop-in API (GaussianRasterizer's autograd function)
+            color, radii, depth, alpha, segment = dgr.rasterize_gaussians(means3D, means2D[0], shs, E, segs, opac,
+                                                                          scales, rots, E, settings[0])
+            state["I"] = color.grad_fn.num_rendered
+            g = torch.autograd.grad([color, depth, alpha, segment], params + means2D, up_list)
+        else:
+            # B views of the step: forward per view, one backward summing the parameter
+            # gradients over the views (gsr_backward_multiview)
+            outs = dgr.rasterize_gaussians_multiview(means3D, means2D, shs, E, segs, opac, scales, rots, E, settings)
+            state["I"] = sum(v[0] for v in outs[0][0].grad_fn.views) / B
+            g = torch.autograd.grad([t for o in outs for t in (o[0], o[2], o[3], o[4])], params + means2D,
+                                    up_list * B)
         if dist is not None:
             dp.allreduce_bucket(dp.arena_of(g[0]), P, shs.shape[1])
         return g
@@ -210,13 +229,13 @@ def main():
             avg = sms[i] / scnt[i]
             stages[names[i]] = {"avg_ms": round(avg, 4), "ms_per_step": round(sms[i] / n_stage_steps, 4),
                                 "launches_per_step": scnt[i] / n_stage_steps,
-                                "gbs": round(algorithmic_bytes(names[i], P, I, HW, deg) / (avg * 1e-3) / 1e9, 1)}
+                                "gbs": round(algorithmic_bytes(names[i], P, I, HW, deg, B) / (avg * 1e-3) / 1e9, 1)}
     dom = names[dom_i] if stages else None
-    value = world * args.steps / elapsed
+    value = world * B * args.steps / elapsed
     roof = None
     if dom and cnt[dom_i]:
         avg_live = ms[dom_i] / cnt[dom_i]  # measured inside the timed region
-        achieved = round(algorithmic_bytes(dom, P, I, HW, deg) / (avg_live * 1e-3) / 1e9, 1)
+        achieved = round(algorithmic_bytes(dom, P, I, HW, deg, B) / (avg_live * 1e-3) / 1e9, 1)
         traffic = valu_frac = None
         if os.path.exists(PMC_SUMMARY):
             try:
@@ -229,7 +248,7 @@ def main():
                 traffic = valu_frac = None
         roof = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg),
+                "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg, B),
                 "avg_launch_ms": round(avg_live, 4), "launches_timed": int(cnt[dom_i]),
                 "valu_issue_frac": valu_frac,
                 "whole_view_frac": round(view_bytes(P, I, HW, deg) * value / world / 1e9 / HBM_PEAK_GBS, 4)}
@@ -239,14 +258,36 @@ def main():
         "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic (SURVEY.md s8d generator, seed 0; upstream grads "
                                                     "N(0,1)*1e-3 seed 1)",
-        "config": {"workload": f"{args.config}: P={P} Gaussians, SH{deg}, {W}x{H}, fwd+bwd per view at the "
-                               f"GaussianRasterizer boundary", "P": P, "width": W, "height": H, "sh_degree": deg,
-                   "num_classes": 2, "num_rendered": I, "global_batch": world, "views_per_step_per_gpu": 1,
+        "config": {"workload": f"{args.config}: P={P} Gaussians, SH{deg}, {W}x{H}, fwd+bwd per view; {B} views per "
+                               f"rank per step" + (" (per-view forward, one multi-view backward)" if B > 1 else
+                                                   " (drop-in GaussianRasterizer)"), "P": P, "width": W, "height": H, "sh_degree": deg,
+                   "num_classes": 2, "num_rendered": I, "global_batch": world * B, "views_per_step_per_gpu": B,
                    "parallelism": f"dp{world}" + (" (views sharded; RCCL all-reduce of the 61 f32/Gaussian "
                                                   "grad bucket per step)" if world > 1 else "")},
         "roofline": roof,
         "stages": stages,
     }
+    out["drop_in_single_view"] = None
+    if rank == 0 and world == 1 and B > 1 and not args.no_train:
+        # the reference's call pattern: one view per forward/backward through the drop-in
+        # GaussianRasterizer autograd function (no multi-view batching)
+        def single():
+            color, radii, depth, alpha, segment = dgr.rasterize_gaussians(means3D, means2D[0], shs, E, segs, opac,
+                                                                          scales, rots, E, settings[0])
+            torch.autograd.grad([color, depth, alpha, segment], params + [means2D[0]], up_list)
+        for _ in range(3):
+            single()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        n_single = max(10, args.steps)
+        for _ in range(n_single):
+            single()
+        torch.cuda.synchronize()
+        el1 = time.perf_counter() - t1
+        out["drop_in_single_view"] = {"value": round(n_single / el1, 2), "unit": "views/s",
+                                      "ms_per_view": round(1e3 * el1 / n_single, 4), "views": n_single,
+                                      "note": "one view per call through GaussianRasterizer (the reference's "
+                                              "pattern), same scene and camera 0"}
     out["train_step"] = None
     if rank == 0 and world == 1 and not args.no_train:
         from gsr_tools import train_bench

@@ -129,6 +129,34 @@ GSR_API int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int*
                  const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
                  const float* dL_dalpha, void* scratch, const gsr_grads* grads, void* stream);
 
+/* ---- multi-view backward: the parameter gradients of B views of the same
+ * Gaussians, SUMMED over the views, in one call (the data-parallel trainer's
+ * per-step batch).  Each view is a completed gsr_forward_* call with
+ * its own settings (camera / image size; P, D and M must be equal) and upstream
+ * gradients.  Equivalent to calling gsr_backward per view and adding the results
+ * (tests/test_gpu_multiview.py), but the per-Gaussian part reads the shared
+ * inputs (means, scales, rotations, SH rows) and writes the parameter gradients
+ * once per batch instead of once per view.  dmeans2D stays per view (the
+ * densification statistics are per view).  grads->dmeans2D is ignored. */
+#define GSR_MAX_VIEWS 16
+typedef struct gsr_view_state {
+    const gsr_settings* s;
+    const int* radii;
+    void* geom;
+    void* binning;
+    void* img;
+    int num_rendered;
+    const float* alpha;
+    const float* dL_dcolor;
+    const float* dL_dsegment;
+    const float* dL_ddepth;
+    const float* dL_dalpha;
+    void* scratch;    /* gsr_backward_scratch_bytes(num_rendered) */
+    float* dmeans2D;  /* [P,3] this view's screen-space gradient, or NULL */
+} gsr_view_state;
+GSR_API size_t gsr_multiview_scratch_bytes(int P, int B);
+GSR_API int gsr_backward_multiview(int B, const gsr_view_state* views, const gsr_inputs* in, void* mv_scratch,
+                                   const gsr_grads* grads, void* stream);
 /* ---- frustum visibility: present[i] = (view-space z > 0.2).  Replaces
  * markVisible (rasterize_points.cu:223-242, rasterizer_impl.cu:54-66). */
 GSR_API int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

@@ -1,0 +1,130 @@
+"""Multi-view backward (include/gsr.h gsr_backward_multiview): the parameter
+gradients of a batch of views in one call must equal the sum of the single-view
+drop-in gradients, and each view's dmeans2D must equal that view's own.
+
+Tolerance: the sums over views are taken in a different order (per-view transforms
+of summed terms vs sums of per-view results; dscales/drot from the summed dcov3D),
+so parameter gradients agree to fp32 rounding: normwise |diff| <= 1e-5 * |ref| per
+tensor.  dmeans2D runs the identical per-view code: bit-exact."""
+import numpy as np
+import pytest
+import torch
+
+import harness as Hn
+from gsr_tools.scene import synthetic_scene, orbit_camera
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def _leaves(scene, colors=False, cov=False, sh_take=None):
+    L = lambda t: t.detach().to(DEV).clone().requires_grad_(True)
+    d = {"means3D": L(scene.means3D), "opacities": L(scene.opacities), "segments": L(scene.segments)}
+    if colors:
+        d["colors_precomp"] = L(torch.rand(scene.P, 3, generator=torch.Generator().manual_seed(5)))
+    else:
+        shs = scene.shs if sh_take is None else scene.shs[:, :sh_take].contiguous()
+        d["shs"] = L(shs)
+    if cov:
+        g = torch.Generator().manual_seed(6)
+        A = torch.randn(scene.P, 3, 3, generator=g) * 0.01
+        C = A @ A.transpose(1, 2) + torch.eye(3) * 1e-5
+        d["cov3D_precomp"] = L(C[:, [0, 0, 0, 1, 1, 2], [0, 1, 2, 1, 2, 2]].contiguous())
+    else:
+        d["scales"], d["rotations"] = L(scene.scales), L(scene.rotations)
+    return d
+
+
+def _views(n, deg, W=160, H=120):
+    cams = [orbit_camera(i, W, H, 150.0, n_views=max(n, 3)) for i in range(n)]
+    return [(Hn.settings_for(c, deg, DEV), Hn.upstream_grads(H, W, seed=10 + i)) for i, c in enumerate(cams)]
+
+
+def _kw(d):
+    E = torch.Tensor([])
+    return dict(sh=d.get("shs", E), colors_precomp=d.get("colors_precomp", E), segments=d["segments"],
+                opacities=d["opacities"], scales=d.get("scales", E), rotations=d.get("rotations", E),
+                cov3Ds_precomp=d.get("cov3D_precomp", E))
+
+
+def _single(d, views):
+    from diff_gaussian_rasterization import rasterize_gaussians
+    total, d2 = {}, []
+    for st, ups in views:
+        m2 = torch.zeros_like(d["means3D"], requires_grad=True)
+        color, radii, depth, alpha, seg = rasterize_gaussians(d["means3D"], m2, raster_settings=st, **_kw(d))
+        grads = torch.autograd.grad([color, depth, alpha, seg], [d[k] for k in d] + [m2],
+                                    [ups["color"].to(DEV), ups["depth"].to(DEV), ups["alpha"].to(DEV),
+                                     ups["segment"].to(DEV)], allow_unused=True)
+        for k, gr in zip(d, grads[:-1]):
+            if gr is not None:
+                total[k] = total.get(k, 0) + gr.double()
+        d2.append(grads[-1])
+    return total, d2
+
+
+def _multi(d, views):
+    from diff_gaussian_rasterization import rasterize_gaussians_multiview
+    m2s = [torch.zeros_like(d["means3D"], requires_grad=True) for _ in views]
+    outs = rasterize_gaussians_multiview(d["means3D"], m2s, raster_settings_list=[v[0] for v in views], **_kw(d))
+    tensors, gouts = [], []
+    for (color, radii, depth, alpha, seg), (_, ups) in zip(outs, views):
+        tensors += [color, depth, alpha, seg]
+        gouts += [ups["color"].to(DEV), ups["depth"].to(DEV), ups["alpha"].to(DEV), ups["segment"].to(DEV)]
+    grads = torch.autograd.grad(tensors, [d[k] for k in d] + m2s, gouts, allow_unused=True)
+    n = len(d)
+    return dict(zip(d, grads[:n])), list(grads[n:]), outs
+
+
+def _check(d, views):
+    ref, ref_d2 = _single(d, views)
+    got, got_d2, outs = _multi(d, views)
+    for k, r in ref.items():
+        g = got[k].double()
+        err = float((g - r).norm() / max(float(r.norm()), 1e-30))
+        assert err <= 1e-5, f"{k}: normwise error {err:.2e}"
+    for v, (a, b) in enumerate(zip(got_d2, ref_d2)):
+        assert torch.equal(a, b), f"view {v}: dmeans2D differs (max {float((a - b).abs().max()):.3e})"
+    return outs
+
+
+@pytest.mark.parametrize("n_views", [1, 3, 8])
+def test_multiview_equals_sum_of_views_sh3(gpu_available, n_views):
+    scene = synthetic_scene(6000, sh_degree=3, seed=41)
+    _check(_leaves(scene), _views(n_views, 3))
+
+
+def test_multiview_forward_outputs_equal_single(gpu_available):
+    from diff_gaussian_rasterization import rasterize_gaussians
+    scene = synthetic_scene(3000, sh_degree=3, seed=42)
+    d = _leaves(scene)
+    views = _views(2, 3)
+    outs = _check(d, views)
+    for (st, _), o in zip(views, outs):
+        r = rasterize_gaussians(d["means3D"], torch.zeros_like(d["means3D"]), raster_settings=st, **_kw(d))
+        for a, b in zip(o, r):
+            assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("variant", ["colors_cov", "sh_deg1_m16", "sh_m9_unstaged"])
+def test_multiview_argument_paths(gpu_available, variant):
+    if variant == "colors_cov":
+        scene = synthetic_scene(4000, sh_degree=3, seed=43)
+        d, views = _leaves(scene, colors=True, cov=True), _views(3, 3)
+    elif variant == "sh_deg1_m16":
+        scene = synthetic_scene(4000, sh_degree=3, seed=44)
+        d, views = _leaves(scene), _views(3, 1)
+    else:
+        scene = synthetic_scene(4000, sh_degree=2, seed=45)  # M = 9: rows of 27 floats, per-thread path
+        d, views = _leaves(scene), _views(3, 2)
+    _check(d, views)
+
+
+def test_multiview_view_with_nothing_visible(gpu_available):
+    scene = synthetic_scene(2000, sh_degree=3, seed=46)
+    d = _leaves(scene)
+    views = _views(2, 3)
+    import copy
+    far = orbit_camera(0, 160, 120, 150.0, radius=-4.0)  # camera behind the scene, looking away
+    views.append((Hn.settings_for(far, 3, DEV), Hn.upstream_grads(120, 160, seed=99)))
+    _check(d, views)
