@@ -1,16 +1,18 @@
 #!/usr/bin/env python
 """bench.py -- forward+backward views/s of the gsr rasterizer (BASELINE.json metric).
 
-One step = the batch of a view-parallel trainer: every rank renders B views
-(--views-per-gpu, default 8) of the replicated synthetic metric scene (1M
-Gaussians, SH3, 2 segment classes, 1920x1080, resident in HBM) -- per view the
-forward at the boundary (incl. the reference's num_rendered host sync) -- then ONE
-backward of the B views with fixed synthetic upstream gradients
-that sums the parameter gradients over them (gsr_backward_multiview), and with N
-GPUs (torchrun, one process per GPU) one RCCL all-reduce of the parameter-gradient
-bucket (61 f32 / Gaussian) per step.  value = N * B * steps / max-over-ranks
-elapsed (weak scaling in views).  --views-per-gpu 1 times the drop-in single-view
-API alone; at N = 1 the default run also reports it as `drop_in_single_view`.
+One step = one view per rank through the drop-in boundary (N views
+per iteration at N GPUs): _RasterizeGaussians.forward (incl. the reference's
+num_rendered host sync) + .backward with fixed synthetic upstream gradients
+(SURVEY.md s8d), on the synthetic metric scene (1M Gaussians, SH3, 2 segment
+classes, 1920x1080) resident in HBM.  With N GPUs (torchrun, one process per GPU)
+every rank renders its own view of the replicated scene and the parameter-gradient
+bucket (61 f32 / Gaussian) is summed with one RCCL all-reduce per step, issued
+asynchronously on RCCL's stream so that it overlaps the next step's render (the
+metric excludes the optimizer step; every exchange completes inside the timed
+region).  value = N * steps / max-over-ranks elapsed (weak scaling in views).
+`batched` additionally times steps of 8 views per rank with one multi-view
+backward and one exchange per step (--views-per-gpu sets the main mode).
 
 Prints ONE JSON line on rank 0.  Extra objects:
   roofline     -- the dominant kernel (per-stage HIP events recorded by libgsr on
@@ -107,9 +109,11 @@ def main():
     ap.add_argument("--cpu-budget", type=float, default=20.0, help="seconds of CPU-oracle work for cpu_baseline")
     ap.add_argument("--stages", action="store_true", help="print the per-stage table to stderr")
     ap.add_argument("--no-train", action="store_true", help="skip the train_step measurement (SURVEY.md s8f)")
-    ap.add_argument("--views-per-gpu", type=int, default=8,
-                    help="views per rank per step (1: the drop-in single-view API; >1: one multi-view backward "
-                         "and one gradient all-reduce per step)")
+    ap.add_argument("--views-per-gpu", type=int, default=1,
+                    help="views per rank per step (1: the drop-in single-view API, BASELINE.md's N views per "
+                         "iteration at N GPUs; >1: one multi-view backward and one all-reduce per step)")
+    ap.add_argument("--batched-views", type=int, default=8,
+                    help="also time steps of this many views per rank (reported under 'batched'; 1 = skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -138,10 +142,12 @@ def main():
     from diff_gaussian_rasterization import _C
 
     B = max(1, min(args.views_per_gpu, 16))
-    n_views = max(8, world * B)
-    scene_cpu, cam_cpu = config_scene_and_camera(args.config, view_index=rank * B, n_views=n_views)
-    cams_cpu = [cam_cpu] + [config_scene_and_camera(args.config, view_index=rank * B + j, n_views=n_views, P=1)[1]
-                            for j in range(1, B)]
+    BB = max(1, min(args.batched_views, 16))  # the extra batched measurement
+    NV = max(B, BB)
+    n_views = max(8, world * NV)
+    scene_cpu, cam_cpu = config_scene_and_camera(args.config, view_index=rank * NV, n_views=n_views)
+    cams_cpu = [cam_cpu] + [config_scene_and_camera(args.config, view_index=rank * NV + j, n_views=n_views, P=1)[1]
+                            for j in range(1, NV)]
     P, W, H, deg = scene_cpu.P, cam_cpu.width, cam_cpu.height, scene_cpu.sh_degree
     gen = torch.Generator().manual_seed(1)
     ups_cpu = {k: (torch.randn(c, H, W, generator=gen) * 1e-3) for k, c in
@@ -150,7 +156,7 @@ def main():
     leaf = lambda t: t.to(device).contiguous().requires_grad_(True)
     means3D, shs, opac = leaf(scene_cpu.means3D), leaf(scene_cpu.shs), leaf(scene_cpu.opacities)
     scales, rots, segs = leaf(scene_cpu.scales), leaf(scene_cpu.rotations), leaf(scene_cpu.segments)
-    means2D = [torch.zeros_like(means3D, requires_grad=True) for _ in range(B)]
+    means2D = [torch.zeros_like(means3D, requires_grad=True) for _ in range(NV)]
     E = torch.empty(0, device=device)
     settings = [dgr.GaussianRasterizationSettings(
         image_height=H, image_width=W, tanfovx=c.tanfovx, tanfovy=c.tanfovy,
@@ -162,26 +168,67 @@ def main():
     state = {"I": 0}
     up_list = [ups["color"], ups["depth"], ups["alpha"], ups["segment"]]
 
-    def step():
-        if B == 1:
-            # one view through the drop-in API (GaussianRasterizer's autograd function)
-            color, radii, depth, alpha, segment = dgr.rasterize_gaussians(means3D, means2D[0], shs, E, segs, opac,
-                                                                          scales, rots, E, settings[0])
-            state["I"] = color.grad_fn.num_rendered
-            g = torch.autograd.grad([color, depth, alpha, segment], params + means2D, up_list)
-        else:
-            # B views of the step: forward per view, one backward summing the parameter
-            # gradients over the views (gsr_backward_multiview)
-            outs = dgr.rasterize_gaussians_multiview(means3D, means2D, shs, E, segs, opac, scales, rots, E, settings)
-            state["I"] = sum(v[0] for v in outs[0][0].grad_fn.views) / B
-            g = torch.autograd.grad([t for o in outs for t in (o[0], o[2], o[3], o[4])], params + means2D,
-                                    up_list * B)
+    pending = []  # the exchange in flight: (work handle, gradients kept alive)
+
+    def exchange(g):
+        # One RCCL all-reduce of the gradient bucket per step, on RCCL's stream: it runs
+        # while the next step renders (the metric excludes the optimizer step, so no
+        # later work waits for it); at most one exchange is in flight.
+        if dist is None:
+            return
+        while pending:
+            pending.pop()[0].wait()
+        h = dist.all_reduce(dp.bucket(dp.arena_of(g[0]), P, shs.shape[1]), op=dist.ReduceOp.SUM, async_op=True)
+        pending.append((h, g))
+
+    def drain():
+        while pending:
+            pending.pop()[0].wait()
+
+    def make_step(nv):
+        def step():
+            if nv == 1:
+                # one view through the drop-in API (GaussianRasterizer's autograd function)
+                color, radii, depth, alpha, segment = dgr.rasterize_gaussians(means3D, means2D[0], shs, E, segs,
+                                                                              opac, scales, rots, E, settings[0])
+                state["I"] = color.grad_fn.num_rendered
+                g = torch.autograd.grad([color, depth, alpha, segment], params + means2D[:1], up_list)
+            else:
+                # nv views: forward per view, one backward summing the parameter gradients
+                # over the views (gsr_backward_multiview)
+                outs = dgr.rasterize_gaussians_multiview(means3D, means2D[:nv], shs, E, segs, opac, scales, rots,
+                                                         E, settings[:nv])
+                state["I"] = sum(v[0] for v in outs[0][0].grad_fn.views) / nv
+                g = torch.autograd.grad([t for o in outs for t in (o[0], o[2], o[3], o[4])],
+                                        params + means2D[:nv], up_list * nv)
+            exchange(g)
+            return g
+        return step
+
+    step = make_step(B)
+
+    def timed(fn, k):
+        """k steps between a barrier + device sync on both sides; max over ranks."""
         if dist is not None:
-            dp.allreduce_bucket(dp.arena_of(g[0]), P, shs.shape[1])
-        return g
+            dist.barrier()
+        torch.cuda.synchronize()
+        t_start = time.perf_counter()
+        for _ in range(k):
+            fn()
+        drain()
+        torch.cuda.synchronize()
+        if dist is not None:
+            dist.barrier()
+        el = time.perf_counter() - t_start
+        if dist is not None:
+            t = torch.tensor([el], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
     for _ in range(args.warmup):
         step()
+    drain()
     torch.cuda.synchronize()
     nst = _C._lib.gsr_num_stages()
     import ctypes
@@ -201,27 +248,15 @@ def main():
     _C._lib.gsr_timing_enable(-1)
     for _ in range(n_stage_steps):
         step()
+    drain()
     torch.cuda.synchronize()
     _C._lib.gsr_timing_enable(0)
     sms, scnt = collect()
     dom_i = max(range(nst), key=lambda i: sms[i]) if any(scnt) else 0
     _C._lib.gsr_timing_enable(1 << dom_i)
-    if dist is not None:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if dist is not None:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
+    elapsed = timed(step, args.steps)
     _C._lib.gsr_timing_enable(0)
     ms, cnt = collect()  # the dominant stage's launches inside the timed region
-    if dist is not None:
-        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
     I, HW = int(state["I"]), W * H
     stages = {}
     for i in range(nst):
@@ -258,36 +293,31 @@ def main():
         "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f32", "data": "synthetic (SURVEY.md s8d generator, seed 0; upstream grads "
                                                     "N(0,1)*1e-3 seed 1)",
-        "config": {"workload": f"{args.config}: P={P} Gaussians, SH{deg}, {W}x{H}, fwd+bwd per view; {B} views per "
+        "config": {"workload": f"{args.config}: P={P} Gaussians, SH{deg}, {W}x{H}, fwd+bwd per view; {B} view(s) per "
                                f"rank per step" + (" (per-view forward, one multi-view backward)" if B > 1 else
-                                                   " (drop-in GaussianRasterizer)"), "P": P, "width": W, "height": H, "sh_degree": deg,
+                                                   " through the drop-in GaussianRasterizer"), "P": P, "width": W, "height": H, "sh_degree": deg,
                    "num_classes": 2, "num_rendered": I, "global_batch": world * B, "views_per_step_per_gpu": B,
-                   "parallelism": f"dp{world}" + (" (views sharded; RCCL all-reduce of the 61 f32/Gaussian "
-                                                  "grad bucket per step)" if world > 1 else "")},
+                   "parallelism": f"dp{world}" + (" (views sharded; one RCCL all-reduce of the 61 f32/Gaussian "
+                                                  "grad bucket per step, overlapped with the next step's "
+                                                  "render)" if world > 1 else "")},
         "roofline": roof,
         "stages": stages,
     }
-    out["drop_in_single_view"] = None
-    if rank == 0 and world == 1 and B > 1 and not args.no_train:
-        # the reference's call pattern: one view per forward/backward through the drop-in
-        # GaussianRasterizer autograd function (no multi-view batching)
-        def single():
-            color, radii, depth, alpha, segment = dgr.rasterize_gaussians(means3D, means2D[0], shs, E, segs, opac,
-                                                                          scales, rots, E, settings[0])
-            torch.autograd.grad([color, depth, alpha, segment], params + [means2D[0]], up_list)
-        for _ in range(3):
-            single()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        n_single = max(10, args.steps)
-        for _ in range(n_single):
-            single()
-        torch.cuda.synchronize()
-        el1 = time.perf_counter() - t1
-        out["drop_in_single_view"] = {"value": round(n_single / el1, 2), "unit": "views/s",
-                                      "ms_per_view": round(1e3 * el1 / n_single, 4), "views": n_single,
-                                      "note": "one view per call through GaussianRasterizer (the reference's "
-                                              "pattern), same scene and camera 0"}
+    out["batched"] = None
+    if BB > 1 and BB != B:
+        # The same hot path with a batch of BB views per rank per step: per-view forward,
+        # one multi-view backward and one exchange per step (bigger, fewer collectives
+        # for point-to-point xGMI; SURVEY.md s8e / DESIGN.md s7).
+        bstep = make_step(BB)
+        for _ in range(max(1, args.warmup // 4)):
+            bstep()
+        drain()
+        k = max(2, args.steps // BB)
+        el_b = timed(bstep, k)
+        out["batched"] = {"views_per_step_per_gpu": BB, "global_batch": world * BB, "steps": k,
+                          "value": round(world * BB * k / el_b, 2), "unit": "views/s",
+                          "ms_per_step": round(1e3 * el_b / k, 4),
+                          "note": "per-view forward + one gsr_backward_multiview over the batch + one all-reduce"}
     out["train_step"] = None
     if rank == 0 and world == 1 and not args.no_train:
         from gsr_tools import train_bench
