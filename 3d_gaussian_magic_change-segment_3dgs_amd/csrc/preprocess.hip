@@ -377,264 +377,265 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         if (g.dsegments) { g.dsegments[2 * (size_t)idx] = 0.f; g.dsegments[2 * (size_t)idx + 1] = 0.f; }
     }
     if (vis) {
-    // gather-sum of the written instance records of the Gaussian's slot range
-    // [goff, goff + tiles_touched), in slot order (deterministic).
-    const float4 r0 = rec[(size_t)idx * REC_F4], r1 = rec[(size_t)idx * REC_F4 + 1];
-    float q[12];
+        // gather-sum of the written instance records of the Gaussian's slot range
+        // [goff, goff + tiles_touched), in slot order (deterministic).
+        const float4 r0 = rec[(size_t)idx * REC_F4], r1 = rec[(size_t)idx * REC_F4 + 1];
+        float q[12];
 #pragma unroll
-    for (int j = 0; j < 12; ++j) q[j] = 0.f;
-    {
-        const uint32_t lo = goff[idx], hi = lo + tiles_touched[idx];
-        for (uint32_t w = lo >> 5; w <= (hi - 1) >> 5; ++w) {
-            uint32_t bits = written[w];
-            if (w == lo >> 5) bits &= ~0u << (lo & 31);
-            if (w == (hi - 1) >> 5 && ((hi & 31) != 0)) bits &= ~(~0u << (hi & 31));
-            while (bits) {
-                const uint32_t u = (w << 5) + (uint32_t)__builtin_ctz(bits);
-                bits &= bits - 1;
-                const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)u * 12);
-                const float4 a = src[0], b = src[1], c = src[2];
-                q[0] += a.x; q[1] += a.y; q[2] += a.z; q[3] += a.w;
-                q[4] += b.x; q[5] += b.y; q[6] += b.z; q[7] += b.w;
-                q[8] += c.x; q[9] += c.y; q[10] += c.z; q[11] += c.w;
-            }
-        }
-    }
-    const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
-    const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * s.W);
-    const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * s.H);
-    if (g.dmeans2D) { g.dmeans2D[i3] = dm2x; g.dmeans2D[i3 + 1] = dm2y; g.dmeans2D[i3 + 2] = 0.f; }
-    if (g.dcolors) { g.dcolors[i3] = q[0]; g.dcolors[i3 + 1] = q[1]; g.dcolors[i3 + 2] = q[2]; }
-    if (g.dopacity) g.dopacity[idx] = q[6];
-    if (g.dsegments) { g.dsegments[2 * (size_t)idx] = q[3]; g.dsegments[2 * (size_t)idx + 1] = q[4]; }
-
-    Cam cam;
-    load_cam(s, cam);
-    const float focal_y = s.H / (2.0f * s.tanfovy);
-    const float focal_x = s.W / (2.0f * s.tanfovx);
-    const f3 mean = ld3(in.means3D + i3);
-
-    // ---- computeCov2DCUDA (backward.cu:155-273)
-    float c3[6];
-    float4 quat = make_float4(0.f, 0.f, 0.f, 0.f);
-    f3 scale = {0.f, 0.f, 0.f};
-    if (in.cov3D_precomp) {
-#pragma unroll
-        for (int i = 0; i < 6; ++i) c3[i] = in.cov3D_precomp[6 * (size_t)idx + i];
-    } else {
-        quat = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)idx);
-        scale = ld3(in.scales + i3);
-        cov3d_from(scale, s.scale_modifier, quat, c3);  // == the forward's geom.cov3D
-    }
-    const float dcx = -0.5f * op * q[9], dcy = -0.5f * op * q[10], dcz = -0.5f * op * q[11];
-    const EwaTerms e = ewa_terms(mean, focal_x, focal_y, s.tanfovx, s.tanfovy, cam.view);
-    const float x_grad_mul = e.txtz < -e.limx || e.txtz > e.limx ? 0 : 1;
-    const float y_grad_mul = e.tytz < -e.limy || e.tytz > e.limy ? 0 : 1;
-    const M3 Vrk = vrk_of(c3);
-    const M3& T = e.T;
-    const M3 cov2D = mmul(mmul(mtr(T), mtr(Vrk)), T);
-    const float a = cov2D.m[0][0] + 0.3f;
-    const float b = cov2D.m[0][1];
-    const float c = cov2D.m[1][1] + 0.3f;
-    const float denom = a * c - b * b;
-    float dL_da = 0, dL_db = 0, dL_dc = 0;
-    const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
-    float dcv[6] = {0, 0, 0, 0, 0, 0};
-    const auto& Tt = T.m;
-    if (denom2inv != 0) {
-        dL_da = denom2inv * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
-        dL_dc = denom2inv * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
-        dL_db = denom2inv * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
-        dcv[0] = (Tt[0][0] * Tt[0][0] * dL_da + Tt[0][0] * Tt[1][0] * dL_db + Tt[1][0] * Tt[1][0] * dL_dc);
-        dcv[3] = (Tt[0][1] * Tt[0][1] * dL_da + Tt[0][1] * Tt[1][1] * dL_db + Tt[1][1] * Tt[1][1] * dL_dc);
-        dcv[5] = (Tt[0][2] * Tt[0][2] * dL_da + Tt[0][2] * Tt[1][2] * dL_db + Tt[1][2] * Tt[1][2] * dL_dc);
-        dcv[1] = 2 * Tt[0][0] * Tt[0][1] * dL_da + (Tt[0][0] * Tt[1][1] + Tt[0][1] * Tt[1][0]) * dL_db +
-                 2 * Tt[1][0] * Tt[1][1] * dL_dc;
-        dcv[2] = 2 * Tt[0][0] * Tt[0][2] * dL_da + (Tt[0][0] * Tt[1][2] + Tt[0][2] * Tt[1][0]) * dL_db +
-                 2 * Tt[1][0] * Tt[1][2] * dL_dc;
-        dcv[4] = 2 * Tt[0][2] * Tt[0][1] * dL_da + (Tt[0][1] * Tt[1][2] + Tt[0][2] * Tt[1][1]) * dL_db +
-                 2 * Tt[1][1] * Tt[1][2] * dL_dc;
-    }
-    const auto& V = Vrk.m;
-    const float dL_dT00 = 2 * (Tt[0][0] * V[0][0] + Tt[0][1] * V[0][1] + Tt[0][2] * V[0][2]) * dL_da +
-                          (Tt[1][0] * V[0][0] + Tt[1][1] * V[0][1] + Tt[1][2] * V[0][2]) * dL_db;
-    const float dL_dT01 = 2 * (Tt[0][0] * V[1][0] + Tt[0][1] * V[1][1] + Tt[0][2] * V[1][2]) * dL_da +
-                          (Tt[1][0] * V[1][0] + Tt[1][1] * V[1][1] + Tt[1][2] * V[1][2]) * dL_db;
-    const float dL_dT02 = 2 * (Tt[0][0] * V[2][0] + Tt[0][1] * V[2][1] + Tt[0][2] * V[2][2]) * dL_da +
-                          (Tt[1][0] * V[2][0] + Tt[1][1] * V[2][1] + Tt[1][2] * V[2][2]) * dL_db;
-    const float dL_dT10 = 2 * (Tt[1][0] * V[0][0] + Tt[1][1] * V[0][1] + Tt[1][2] * V[0][2]) * dL_dc +
-                          (Tt[0][0] * V[0][0] + Tt[0][1] * V[0][1] + Tt[0][2] * V[0][2]) * dL_db;
-    const float dL_dT11 = 2 * (Tt[1][0] * V[1][0] + Tt[1][1] * V[1][1] + Tt[1][2] * V[1][2]) * dL_dc +
-                          (Tt[0][0] * V[1][0] + Tt[0][1] * V[1][1] + Tt[0][2] * V[1][2]) * dL_db;
-    const float dL_dT12 = 2 * (Tt[1][0] * V[2][0] + Tt[1][1] * V[2][1] + Tt[1][2] * V[2][2]) * dL_dc +
-                          (Tt[0][0] * V[2][0] + Tt[0][1] * V[2][1] + Tt[0][2] * V[2][2]) * dL_db;
-    const auto& Wt = e.W.m;
-    const float dL_dJ00 = Wt[0][0] * dL_dT00 + Wt[0][1] * dL_dT01 + Wt[0][2] * dL_dT02;
-    const float dL_dJ02 = Wt[2][0] * dL_dT00 + Wt[2][1] * dL_dT01 + Wt[2][2] * dL_dT02;
-    const float dL_dJ11 = Wt[1][0] * dL_dT10 + Wt[1][1] * dL_dT11 + Wt[1][2] * dL_dT12;
-    const float dL_dJ12 = Wt[2][0] * dL_dT10 + Wt[2][1] * dL_dT11 + Wt[2][2] * dL_dT12;
-    const float hx = focal_x, hy = focal_y;
-    const f3 t = e.t;
-    const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
-    const float dL_dtx = x_grad_mul * -hx * tz2 * dL_dJ02;
-    const float dL_dty = y_grad_mul * -hy * tz2 * dL_dJ12;
-    const float dL_dtz = -hx * tz2 * dL_dJ00 - hy * tz2 * dL_dJ11 + (2 * hx * t.x) * tz3 * dL_dJ02 +
-                         (2 * hy * t.y) * tz3 * dL_dJ12;
-    f3 dmean = xformVecT({dL_dtx, dL_dty, dL_dtz}, cam.view);
-    if (g.dcov3D)
-#pragma unroll
-        for (int i = 0; i < 6; ++i) g.dcov3D[6 * (size_t)idx + i] = dcv[i];
-
-    // ---- preprocessCUDA backward (backward.cu:372-411)
-    const float* proj = cam.proj;
-    const float* view = cam.view;
-    const f3 m = mean;
-    const float4 m_hom = xform4x4(m, proj);
-    const float m_w = 1.0f / (m_hom.w + 0.0000001f);
-    const float d2x = dm2x, d2y = dm2y;
-    const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
-    const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
-    f3 dm;
-    dm.x = (proj[0] * m_w - proj[3] * mul1) * d2x + (proj[1] * m_w - proj[3] * mul2) * d2y;
-    dm.y = (proj[4] * m_w - proj[7] * mul1) * d2x + (proj[5] * m_w - proj[7] * mul2) * d2y;
-    dm.z = (proj[8] * m_w - proj[11] * mul1) * d2x + (proj[9] * m_w - proj[11] * mul2) * d2y;
-    dmean = dmean + dm;
-    const float ddepth = q[5];
-    const float mul3 = view[2] * m.x + view[6] * m.y + view[10] * m.z + view[14];
-    f3 dm2;
-    dm2.x = (view[2] - view[3] * mul3) * ddepth;
-    dm2.y = (view[6] - view[7] * mul3) * ddepth;
-    dm2.z = (view[10] - view[11] * mul3) * ddepth;
-    dmean = dmean + dm2;
-
-    if (in.shs) {
-        // computeColorFromSH backward (backward.cu:20-139)
-        const int deg = s.D;
-        ShRow S;
-        S.load(in.shs + (size_t)idx * M * 3, M, (deg + 1) * (deg + 1));
-        const f3 dir_orig = m - cam.campos;
-        const f3 dir = dir_orig / sqrtf(dot3(dir_orig, dir_orig));
-        const uint8_t cb = clamped[idx];
-        f3 dRGB = {q[0], q[1], q[2]};
-        dRGB.x *= (cb & 1) ? 0 : 1;
-        dRGB.y *= (cb & 2) ? 0 : 1;
-        dRGB.z *= (cb & 4) ? 0 : 1;
-        f3 dx = {0, 0, 0}, dy = {0, 0, 0}, dz = {0, 0, 0};
-        const float x = dir.x, y = dir.y, z = dir.z;
-        // dL/dsh[i] = basis_i * dRGB (backward.cu:46-110); coefficients >= (D+1)^2 get 0
-        bas[0] = C_SH0;
-        if (deg > 0) {
-            bas[1] = -C_SH1 * y; bas[2] = C_SH1 * z; bas[3] = -C_SH1 * x;
-            dx = -C_SH1 * S(3);
-            dy = -C_SH1 * S(1);
-            dz = C_SH1 * S(2);
-            if (deg > 1) {
-                const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-                bas[4] = C_SH2[0] * xy;
-                bas[5] = C_SH2[1] * yz;
-                bas[6] = C_SH2[2] * (2.f * zz - xx - yy);
-                bas[7] = C_SH2[3] * xz;
-                bas[8] = C_SH2[4] * (xx - yy);
-                dx = dx + (C_SH2[0] * y * S(4) + C_SH2[2] * 2.f * -x * S(6) + C_SH2[3] * z * S(7) +
-                           C_SH2[4] * 2.f * x * S(8));
-                dy = dy + (C_SH2[0] * x * S(4) + C_SH2[1] * z * S(5) + C_SH2[2] * 2.f * -y * S(6) +
-                           C_SH2[4] * 2.f * -y * S(8));
-                dz = dz + (C_SH2[1] * y * S(5) + C_SH2[2] * 2.f * 2.f * z * S(6) + C_SH2[3] * x * S(7));
-                if (deg > 2) {
-                    bas[9] = C_SH3[0] * y * (3.f * xx - yy);
-                    bas[10] = C_SH3[1] * xy * z;
-                    bas[11] = C_SH3[2] * y * (4.f * zz - xx - yy);
-                    bas[12] = C_SH3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                    bas[13] = C_SH3[4] * x * (4.f * zz - xx - yy);
-                    bas[14] = C_SH3[5] * z * (xx - yy);
-                    bas[15] = C_SH3[6] * x * (xx - 3.f * yy);
-                    dx = dx + (C_SH3[0] * S(9) * 3.f * 2.f * xy + C_SH3[1] * S(10) * yz +
-                               C_SH3[2] * S(11) * -2.f * xy + C_SH3[3] * S(12) * -3.f * 2.f * xz +
-                               C_SH3[4] * S(13) * (-3.f * xx + 4.f * zz - yy) + C_SH3[5] * S(14) * 2.f * xz +
-                               C_SH3[6] * S(15) * 3.f * (xx - yy));
-                    dy = dy + (C_SH3[0] * S(9) * 3.f * (xx - yy) + C_SH3[1] * S(10) * xz +
-                               C_SH3[2] * S(11) * (-3.f * yy + 4.f * zz - xx) + C_SH3[3] * S(12) * -3.f * 2.f * yz +
-                               C_SH3[4] * S(13) * -2.f * xy + C_SH3[5] * S(14) * -2.f * yz +
-                               C_SH3[6] * S(15) * -3.f * 2.f * xy);
-                    dz = dz + (C_SH3[1] * S(10) * xy + C_SH3[2] * S(11) * 4.f * 2.f * yz +
-                               C_SH3[3] * S(12) * 3.f * (2.f * zz - xx - yy) + C_SH3[4] * S(13) * 4.f * 2.f * xz +
-                               C_SH3[5] * S(14) * (xx - yy));
+        for (int j = 0; j < 12; ++j) q[j] = 0.f;
+        {
+            const uint32_t lo = goff[idx], hi = lo + tiles_touched[idx];
+            for (uint32_t w = lo >> 5; w <= (hi - 1) >> 5; ++w) {
+                uint32_t bits = written[w];
+                if (w == lo >> 5) bits &= ~0u << (lo & 31);
+                if (w == (hi - 1) >> 5 && ((hi & 31) != 0)) bits &= ~(~0u << (hi & 31));
+                while (bits) {
+                    const uint32_t u = (w << 5) + (uint32_t)__builtin_ctz(bits);
+                    bits &= bits - 1;
+                    const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)u * 12);
+                    const float4 a = src[0], b = src[1], c = src[2];
+                    q[0] += a.x; q[1] += a.y; q[2] += a.z; q[3] += a.w;
+                    q[4] += b.x; q[5] += b.y; q[6] += b.z; q[7] += b.w;
+                    q[8] += c.x; q[9] += c.y; q[10] += c.z; q[11] += c.w;
                 }
             }
         }
-        dc[0] = dRGB.x;
-        dc[1] = dRGB.y;
-        dc[2] = dRGB.z;
-        if (g.dsh && !stage_dsh) {
-            float* o = g.dsh + (size_t)idx * M * 3;
-            auto val = [&](int f) { return f < 48 ? bas[f / 3] * dc[f % 3] : 0.f; };
-            if (((3 * M) & 3) == 0 && (reinterpret_cast<uintptr_t>(o) & 15) == 0 && M <= 16) {
-                float4* o4 = reinterpret_cast<float4*>(o);
+        const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
+        const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * s.W);
+        const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * s.H);
+        if (g.dmeans2D) { g.dmeans2D[i3] = dm2x; g.dmeans2D[i3 + 1] = dm2y; g.dmeans2D[i3 + 2] = 0.f; }
+        if (g.dcolors) { g.dcolors[i3] = q[0]; g.dcolors[i3 + 1] = q[1]; g.dcolors[i3 + 2] = q[2]; }
+        if (g.dopacity) g.dopacity[idx] = q[6];
+        if (g.dsegments) { g.dsegments[2 * (size_t)idx] = q[3]; g.dsegments[2 * (size_t)idx + 1] = q[4]; }
+
+        Cam cam;
+        load_cam(s, cam);
+        const float focal_y = s.H / (2.0f * s.tanfovy);
+        const float focal_x = s.W / (2.0f * s.tanfovx);
+        const f3 mean = ld3(in.means3D + i3);
+
+        // ---- computeCov2DCUDA (backward.cu:155-273)
+        float c3[6];
+        float4 quat = make_float4(0.f, 0.f, 0.f, 0.f);
+        f3 scale = {0.f, 0.f, 0.f};
+        if (in.cov3D_precomp) {
 #pragma unroll
-                for (int i = 0; i < 12; ++i)
-                    if (4 * i < 3 * M) o4[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
-            } else {
-                for (int f = 0; f < 3 * M; ++f) o[f] = f < 48 ? bas[f / 3] * dc[f % 3] : 0.f;
+            for (int i = 0; i < 6; ++i) c3[i] = in.cov3D_precomp[6 * (size_t)idx + i];
+        } else {
+            quat = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)idx);
+            scale = ld3(in.scales + i3);
+            cov3d_from(scale, s.scale_modifier, quat, c3);  // == the forward's geom.cov3D
+        }
+        const float dcx = -0.5f * op * q[9], dcy = -0.5f * op * q[10], dcz = -0.5f * op * q[11];
+        const EwaTerms e = ewa_terms(mean, focal_x, focal_y, s.tanfovx, s.tanfovy, cam.view);
+        const float x_grad_mul = e.txtz < -e.limx || e.txtz > e.limx ? 0 : 1;
+        const float y_grad_mul = e.tytz < -e.limy || e.tytz > e.limy ? 0 : 1;
+        const M3 Vrk = vrk_of(c3);
+        const M3& T = e.T;
+        const M3 cov2D = mmul(mmul(mtr(T), mtr(Vrk)), T);
+        const float a = cov2D.m[0][0] + 0.3f;
+        const float b = cov2D.m[0][1];
+        const float c = cov2D.m[1][1] + 0.3f;
+        const float denom = a * c - b * b;
+        float dL_da = 0, dL_db = 0, dL_dc = 0;
+        const float denom2inv = 1.0f / ((denom * denom) + 0.0000001f);
+        float dcv[6] = {0, 0, 0, 0, 0, 0};
+        const auto& Tt = T.m;
+        if (denom2inv != 0) {
+            dL_da = denom2inv * (-c * c * dcx + 2 * b * c * dcy + (denom - a * c) * dcz);
+            dL_dc = denom2inv * (-a * a * dcz + 2 * a * b * dcy + (denom - a * c) * dcx);
+            dL_db = denom2inv * 2 * (b * c * dcx - (denom + 2 * b * b) * dcy + a * b * dcz);
+            dcv[0] = (Tt[0][0] * Tt[0][0] * dL_da + Tt[0][0] * Tt[1][0] * dL_db + Tt[1][0] * Tt[1][0] * dL_dc);
+            dcv[3] = (Tt[0][1] * Tt[0][1] * dL_da + Tt[0][1] * Tt[1][1] * dL_db + Tt[1][1] * Tt[1][1] * dL_dc);
+            dcv[5] = (Tt[0][2] * Tt[0][2] * dL_da + Tt[0][2] * Tt[1][2] * dL_db + Tt[1][2] * Tt[1][2] * dL_dc);
+            dcv[1] = 2 * Tt[0][0] * Tt[0][1] * dL_da + (Tt[0][0] * Tt[1][1] + Tt[0][1] * Tt[1][0]) * dL_db +
+                     2 * Tt[1][0] * Tt[1][1] * dL_dc;
+            dcv[2] = 2 * Tt[0][0] * Tt[0][2] * dL_da + (Tt[0][0] * Tt[1][2] + Tt[0][2] * Tt[1][0]) * dL_db +
+                     2 * Tt[1][0] * Tt[1][2] * dL_dc;
+            dcv[4] = 2 * Tt[0][2] * Tt[0][1] * dL_da + (Tt[0][1] * Tt[1][2] + Tt[0][2] * Tt[1][1]) * dL_db +
+                     2 * Tt[1][1] * Tt[1][2] * dL_dc;
+        }
+        const auto& V = Vrk.m;
+        const float dL_dT00 = 2 * (Tt[0][0] * V[0][0] + Tt[0][1] * V[0][1] + Tt[0][2] * V[0][2]) * dL_da +
+                              (Tt[1][0] * V[0][0] + Tt[1][1] * V[0][1] + Tt[1][2] * V[0][2]) * dL_db;
+        const float dL_dT01 = 2 * (Tt[0][0] * V[1][0] + Tt[0][1] * V[1][1] + Tt[0][2] * V[1][2]) * dL_da +
+                              (Tt[1][0] * V[1][0] + Tt[1][1] * V[1][1] + Tt[1][2] * V[1][2]) * dL_db;
+        const float dL_dT02 = 2 * (Tt[0][0] * V[2][0] + Tt[0][1] * V[2][1] + Tt[0][2] * V[2][2]) * dL_da +
+                              (Tt[1][0] * V[2][0] + Tt[1][1] * V[2][1] + Tt[1][2] * V[2][2]) * dL_db;
+        const float dL_dT10 = 2 * (Tt[1][0] * V[0][0] + Tt[1][1] * V[0][1] + Tt[1][2] * V[0][2]) * dL_dc +
+                              (Tt[0][0] * V[0][0] + Tt[0][1] * V[0][1] + Tt[0][2] * V[0][2]) * dL_db;
+        const float dL_dT11 = 2 * (Tt[1][0] * V[1][0] + Tt[1][1] * V[1][1] + Tt[1][2] * V[1][2]) * dL_dc +
+                              (Tt[0][0] * V[1][0] + Tt[0][1] * V[1][1] + Tt[0][2] * V[1][2]) * dL_db;
+        const float dL_dT12 = 2 * (Tt[1][0] * V[2][0] + Tt[1][1] * V[2][1] + Tt[1][2] * V[2][2]) * dL_dc +
+                              (Tt[0][0] * V[2][0] + Tt[0][1] * V[2][1] + Tt[0][2] * V[2][2]) * dL_db;
+        const auto& Wt = e.W.m;
+        const float dL_dJ00 = Wt[0][0] * dL_dT00 + Wt[0][1] * dL_dT01 + Wt[0][2] * dL_dT02;
+        const float dL_dJ02 = Wt[2][0] * dL_dT00 + Wt[2][1] * dL_dT01 + Wt[2][2] * dL_dT02;
+        const float dL_dJ11 = Wt[1][0] * dL_dT10 + Wt[1][1] * dL_dT11 + Wt[1][2] * dL_dT12;
+        const float dL_dJ12 = Wt[2][0] * dL_dT10 + Wt[2][1] * dL_dT11 + Wt[2][2] * dL_dT12;
+        const float hx = focal_x, hy = focal_y;
+        const f3 t = e.t;
+        const float tz = 1.f / t.z, tz2 = tz * tz, tz3 = tz2 * tz;
+        const float dL_dtx = x_grad_mul * -hx * tz2 * dL_dJ02;
+        const float dL_dty = y_grad_mul * -hy * tz2 * dL_dJ12;
+        const float dL_dtz = -hx * tz2 * dL_dJ00 - hy * tz2 * dL_dJ11 + (2 * hx * t.x) * tz3 * dL_dJ02 +
+                             (2 * hy * t.y) * tz3 * dL_dJ12;
+        f3 dmean = xformVecT({dL_dtx, dL_dty, dL_dtz}, cam.view);
+        if (g.dcov3D)
+#pragma unroll
+            for (int i = 0; i < 6; ++i) g.dcov3D[6 * (size_t)idx + i] = dcv[i];
+
+        // ---- preprocessCUDA backward (backward.cu:372-411)
+        const float* proj = cam.proj;
+        const float* view = cam.view;
+        const f3 m = mean;
+        const float4 m_hom = xform4x4(m, proj);
+        const float m_w = 1.0f / (m_hom.w + 0.0000001f);
+        const float d2x = dm2x, d2y = dm2y;
+        const float mul1 = (proj[0] * m.x + proj[4] * m.y + proj[8] * m.z + proj[12]) * m_w * m_w;
+        const float mul2 = (proj[1] * m.x + proj[5] * m.y + proj[9] * m.z + proj[13]) * m_w * m_w;
+        f3 dm;
+        dm.x = (proj[0] * m_w - proj[3] * mul1) * d2x + (proj[1] * m_w - proj[3] * mul2) * d2y;
+        dm.y = (proj[4] * m_w - proj[7] * mul1) * d2x + (proj[5] * m_w - proj[7] * mul2) * d2y;
+        dm.z = (proj[8] * m_w - proj[11] * mul1) * d2x + (proj[9] * m_w - proj[11] * mul2) * d2y;
+        dmean = dmean + dm;
+        const float ddepth = q[5];
+        const float mul3 = view[2] * m.x + view[6] * m.y + view[10] * m.z + view[14];
+        f3 dm2;
+        dm2.x = (view[2] - view[3] * mul3) * ddepth;
+        dm2.y = (view[6] - view[7] * mul3) * ddepth;
+        dm2.z = (view[10] - view[11] * mul3) * ddepth;
+        dmean = dmean + dm2;
+
+        if (in.shs) {
+            // computeColorFromSH backward (backward.cu:20-139)
+            const int deg = s.D;
+            ShRow S;
+            S.load(in.shs + (size_t)idx * M * 3, M, (deg + 1) * (deg + 1));
+            const f3 dir_orig = m - cam.campos;
+            const f3 dir = dir_orig / sqrtf(dot3(dir_orig, dir_orig));
+            const uint8_t cb = clamped[idx];
+            f3 dRGB = {q[0], q[1], q[2]};
+            dRGB.x *= (cb & 1) ? 0 : 1;
+            dRGB.y *= (cb & 2) ? 0 : 1;
+            dRGB.z *= (cb & 4) ? 0 : 1;
+            f3 dx = {0, 0, 0}, dy = {0, 0, 0}, dz = {0, 0, 0};
+            const float x = dir.x, y = dir.y, z = dir.z;
+            // dL/dsh[i] = basis_i * dRGB (backward.cu:46-110); coefficients >= (D+1)^2 get 0
+            bas[0] = C_SH0;
+            if (deg > 0) {
+                bas[1] = -C_SH1 * y; bas[2] = C_SH1 * z; bas[3] = -C_SH1 * x;
+                dx = -C_SH1 * S(3);
+                dy = -C_SH1 * S(1);
+                dz = C_SH1 * S(2);
+                if (deg > 1) {
+                    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+                    bas[4] = C_SH2[0] * xy;
+                    bas[5] = C_SH2[1] * yz;
+                    bas[6] = C_SH2[2] * (2.f * zz - xx - yy);
+                    bas[7] = C_SH2[3] * xz;
+                    bas[8] = C_SH2[4] * (xx - yy);
+                    dx = dx + (C_SH2[0] * y * S(4) + C_SH2[2] * 2.f * -x * S(6) + C_SH2[3] * z * S(7) +
+                               C_SH2[4] * 2.f * x * S(8));
+                    dy = dy + (C_SH2[0] * x * S(4) + C_SH2[1] * z * S(5) + C_SH2[2] * 2.f * -y * S(6) +
+                               C_SH2[4] * 2.f * -y * S(8));
+                    dz = dz + (C_SH2[1] * y * S(5) + C_SH2[2] * 2.f * 2.f * z * S(6) + C_SH2[3] * x * S(7));
+                    if (deg > 2) {
+                        bas[9] = C_SH3[0] * y * (3.f * xx - yy);
+                        bas[10] = C_SH3[1] * xy * z;
+                        bas[11] = C_SH3[2] * y * (4.f * zz - xx - yy);
+                        bas[12] = C_SH3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                        bas[13] = C_SH3[4] * x * (4.f * zz - xx - yy);
+                        bas[14] = C_SH3[5] * z * (xx - yy);
+                        bas[15] = C_SH3[6] * x * (xx - 3.f * yy);
+                        dx = dx + (C_SH3[0] * S(9) * 3.f * 2.f * xy + C_SH3[1] * S(10) * yz +
+                                   C_SH3[2] * S(11) * -2.f * xy + C_SH3[3] * S(12) * -3.f * 2.f * xz +
+                                   C_SH3[4] * S(13) * (-3.f * xx + 4.f * zz - yy) + C_SH3[5] * S(14) * 2.f * xz +
+                                   C_SH3[6] * S(15) * 3.f * (xx - yy));
+                        dy = dy + (C_SH3[0] * S(9) * 3.f * (xx - yy) + C_SH3[1] * S(10) * xz +
+                                   C_SH3[2] * S(11) * (-3.f * yy + 4.f * zz - xx) + C_SH3[3] * S(12) * -3.f * 2.f * yz +
+                                   C_SH3[4] * S(13) * -2.f * xy + C_SH3[5] * S(14) * -2.f * yz +
+                                   C_SH3[6] * S(15) * -3.f * 2.f * xy);
+                        dz = dz + (C_SH3[1] * S(10) * xy + C_SH3[2] * S(11) * 4.f * 2.f * yz +
+                                   C_SH3[3] * S(12) * 3.f * (2.f * zz - xx - yy) + C_SH3[4] * S(13) * 4.f * 2.f * xz +
+                                   C_SH3[5] * S(14) * (xx - yy));
+                    }
+                }
+            }
+            dc[0] = dRGB.x;
+            dc[1] = dRGB.y;
+            dc[2] = dRGB.z;
+            if (g.dsh && !stage_dsh) {
+                float* o = g.dsh + (size_t)idx * M * 3;
+                auto val = [&](int f) { return f < 48 ? bas[f / 3] * dc[f % 3] : 0.f; };
+                if (((3 * M) & 3) == 0 && (reinterpret_cast<uintptr_t>(o) & 15) == 0 && M <= 16) {
+                    float4* o4 = reinterpret_cast<float4*>(o);
+#pragma unroll
+                    for (int i = 0; i < 12; ++i)
+                        if (4 * i < 3 * M)
+                            o4[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
+                } else {
+                    for (int f = 0; f < 3 * M; ++f) o[f] = f < 48 ? bas[f / 3] * dc[f % 3] : 0.f;
+                }
+            }
+            const f3 dL_ddir = {dot3(dx, dRGB), dot3(dy, dRGB), dot3(dz, dRGB)};
+            // dnormvdv (auxiliary.h:107-117)
+            const f3 v = dir_orig, dv = dL_ddir;
+            const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+            const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+            f3 dn;
+            dn.x = ((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32;
+            dn.y = (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32;
+            dn.z = (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32;
+            dmean = dmean + dn;
+        }
+        if (g.dmeans3D) { g.dmeans3D[i3] = dmean.x; g.dmeans3D[i3 + 1] = dmean.y; g.dmeans3D[i3 + 2] = dmean.z; }
+
+        if (in.scales) {
+            // computeCov3D backward (backward.cu:276-341)
+            const float r = quat.x, x = quat.y, y = quat.z, z = quat.w;
+            const M3 R = mat3(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+                              2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+                              2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+            M3 S = mat3(1, 0, 0, 0, 1, 0, 0, 0, 1);
+            const f3 sv = s.scale_modifier * scale;
+            S.m[0][0] = sv.x;
+            S.m[1][1] = sv.y;
+            S.m[2][2] = sv.z;
+            const M3 Mm = mmul(S, R);
+            const M3 dSig = mat3(dcv[0], 0.5f * dcv[1], 0.5f * dcv[2], 0.5f * dcv[1], dcv[3], 0.5f * dcv[4],
+                                 0.5f * dcv[2], 0.5f * dcv[4], dcv[5]);
+            M3 M2;
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc)
+#pragma unroll
+                for (int rr = 0; rr < 3; ++rr) M2.m[cc][rr] = 2.0f * Mm.m[cc][rr];
+            const M3 dM = mmul(M2, dSig);
+            const M3 Rt = mtr(R);
+            M3 dMt = mtr(dM);
+            if (g.dscales) {
+                g.dscales[i3 + 0] = Rt.m[0][0] * dMt.m[0][0] + Rt.m[0][1] * dMt.m[0][1] + Rt.m[0][2] * dMt.m[0][2];
+                g.dscales[i3 + 1] = Rt.m[1][0] * dMt.m[1][0] + Rt.m[1][1] * dMt.m[1][1] + Rt.m[1][2] * dMt.m[1][2];
+                g.dscales[i3 + 2] = Rt.m[2][0] * dMt.m[2][0] + Rt.m[2][1] * dMt.m[2][1] + Rt.m[2][2] * dMt.m[2][2];
+            }
+#pragma unroll
+            for (int rr = 0; rr < 3; ++rr) {
+                dMt.m[0][rr] *= sv.x;
+                dMt.m[1][rr] *= sv.y;
+                dMt.m[2][rr] *= sv.z;
+            }
+            const auto& d = dMt.m;
+            if (g.drot) {
+                float* dr = g.drot + 4 * (size_t)idx;
+                dr[0] = 2 * z * (d[0][1] - d[1][0]) + 2 * y * (d[2][0] - d[0][2]) + 2 * x * (d[1][2] - d[2][1]);
+                dr[1] = 2 * y * (d[1][0] + d[0][1]) + 2 * z * (d[2][0] + d[0][2]) + 2 * r * (d[1][2] - d[2][1]) -
+                        4 * x * (d[2][2] + d[1][1]);
+                dr[2] = 2 * x * (d[1][0] + d[0][1]) + 2 * r * (d[2][0] - d[0][2]) + 2 * z * (d[1][2] + d[2][1]) -
+                        4 * y * (d[2][2] + d[0][0]);
+                dr[3] = 2 * r * (d[0][1] - d[1][0]) + 2 * x * (d[2][0] + d[0][2]) + 2 * y * (d[1][2] + d[2][1]) -
+                        4 * z * (d[1][1] + d[0][0]);
             }
         }
-        const f3 dL_ddir = {dot3(dx, dRGB), dot3(dy, dRGB), dot3(dz, dRGB)};
-        // dnormvdv (auxiliary.h:107-117)
-        const f3 v = dir_orig, dv = dL_ddir;
-        const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
-        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-        f3 dn;
-        dn.x = ((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32;
-        dn.y = (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32;
-        dn.z = (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32;
-        dmean = dmean + dn;
-    }
-    if (g.dmeans3D) { g.dmeans3D[i3] = dmean.x; g.dmeans3D[i3 + 1] = dmean.y; g.dmeans3D[i3 + 2] = dmean.z; }
-
-    if (in.scales) {
-        // computeCov3D backward (backward.cu:276-341)
-        const float r = quat.x, x = quat.y, y = quat.z, z = quat.w;
-        const M3 R = mat3(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
-                          2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
-                          2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
-        M3 S = mat3(1, 0, 0, 0, 1, 0, 0, 0, 1);
-        const f3 sv = s.scale_modifier * scale;
-        S.m[0][0] = sv.x;
-        S.m[1][1] = sv.y;
-        S.m[2][2] = sv.z;
-        const M3 Mm = mmul(S, R);
-        const M3 dSig = mat3(dcv[0], 0.5f * dcv[1], 0.5f * dcv[2], 0.5f * dcv[1], dcv[3], 0.5f * dcv[4],
-                             0.5f * dcv[2], 0.5f * dcv[4], dcv[5]);
-        M3 M2;
-#pragma unroll
-        for (int cc = 0; cc < 3; ++cc)
-#pragma unroll
-            for (int rr = 0; rr < 3; ++rr) M2.m[cc][rr] = 2.0f * Mm.m[cc][rr];
-        const M3 dM = mmul(M2, dSig);
-        const M3 Rt = mtr(R);
-        M3 dMt = mtr(dM);
-        if (g.dscales) {
-            g.dscales[i3 + 0] = Rt.m[0][0] * dMt.m[0][0] + Rt.m[0][1] * dMt.m[0][1] + Rt.m[0][2] * dMt.m[0][2];
-            g.dscales[i3 + 1] = Rt.m[1][0] * dMt.m[1][0] + Rt.m[1][1] * dMt.m[1][1] + Rt.m[1][2] * dMt.m[1][2];
-            g.dscales[i3 + 2] = Rt.m[2][0] * dMt.m[2][0] + Rt.m[2][1] * dMt.m[2][1] + Rt.m[2][2] * dMt.m[2][2];
-        }
-#pragma unroll
-        for (int rr = 0; rr < 3; ++rr) {
-            dMt.m[0][rr] *= sv.x;
-            dMt.m[1][rr] *= sv.y;
-            dMt.m[2][rr] *= sv.z;
-        }
-        const auto& d = dMt.m;
-        if (g.drot) {
-            float* dr = g.drot + 4 * (size_t)idx;
-            dr[0] = 2 * z * (d[0][1] - d[1][0]) + 2 * y * (d[2][0] - d[0][2]) + 2 * x * (d[1][2] - d[2][1]);
-            dr[1] = 2 * y * (d[1][0] + d[0][1]) + 2 * z * (d[2][0] + d[0][2]) + 2 * r * (d[1][2] - d[2][1]) -
-                    4 * x * (d[2][2] + d[1][1]);
-            dr[2] = 2 * x * (d[1][0] + d[0][1]) + 2 * r * (d[2][0] - d[0][2]) + 2 * z * (d[1][2] + d[2][1]) -
-                    4 * y * (d[2][2] + d[0][0]);
-            dr[3] = 2 * r * (d[0][1] - d[1][0]) + 2 * x * (d[2][0] + d[0][2]) + 2 * y * (d[1][2] + d[2][1]) -
-                    4 * z * (d[1][1] + d[0][0]);
-        }
-    }
     }  // vis
     if (stage_dsh) {
         // pass p: lanes 16p..16p+15 of each wave park their rows (padded to 52 floats:
@@ -649,7 +650,8 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
             if ((lane >> 4) == p) {
                 float4* row = srow[wave][lane & 15];
 #pragma unroll
-                for (int i = 0; i < 12; ++i) row[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
+                for (int i = 0; i < 12; ++i)
+                    row[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
             }
             __syncthreads();
             const int g0 = wbase + 16 * p;
@@ -826,7 +828,11 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, floa
 #pragma unroll
         for (int i = 0; i < 6; ++i) g.dcov3D[6 * (size_t)idx + i] = dcv_sum[i];
     // dmeans3D without the SH direction term (k_gaussian_backward_mv_sh adds it)
-    if (g.dmeans3D) { g.dmeans3D[i3] = dmean_sum.x; g.dmeans3D[i3 + 1] = dmean_sum.y; g.dmeans3D[i3 + 2] = dmean_sum.z; }
+    if (g.dmeans3D) {
+        g.dmeans3D[i3] = dmean_sum.x;
+        g.dmeans3D[i3 + 1] = dmean_sum.y;
+        g.dmeans3D[i3 + 2] = dmean_sum.z;
+    }
     if (in.scales) {
         // computeCov3D backward (backward.cu:276-341) of the summed dcov3D (linear in it)
         const float* dcv = dcv_sum;
