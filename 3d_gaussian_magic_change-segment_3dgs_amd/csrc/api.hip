@@ -366,13 +366,19 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
 }
 
 size_t gsr_multiview_scratch_bytes(int P, int B) {
-    return gsr::align_up((size_t)(P > 0 ? P : 0) * (size_t)(B > 0 ? B : 0) * 16) + gsr::ALIGN;
+    return gsr::align_up(gsr::sh_rows_floats(P > 0 ? P : 0) * (size_t)(B > 0 ? B : 0) * 4) + gsr::ALIGN;
 }
 
-int gsr_backward_multiview(int B, const gsr_view_state* views, const gsr_inputs* in, void* mv_scratch,
-                           const gsr_grads* grads, void* stream) {
+size_t gsr_sh_rows_floats(int P) { return gsr::sh_rows_floats(P > 0 ? P : 0); }
+
+namespace {
+int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs* in, void* mv_scratch,
+                            float* sh_rows, const gsr_grads* grads, void* stream) {
     using namespace gsr;
     g_last_error.clear();
+    const bool defer = sh_rows != nullptr;
+    if (defer && (!in || !in->shs)) return fail("[gsr] deferred SH backward: shs must be present");
+    if (defer && (reinterpret_cast<uintptr_t>(sh_rows) & 15)) return fail("[gsr] deferred SH backward: sh_rows must be 16-B aligned");
     if (B < 1 || B > GSR_MAX_VIEWS) return fail("[gsr] multiview: B must be 1..16");
     if (!views || !in || !grads) return fail("[gsr] multiview: null argument");
     const gsr_settings* s0 = views[0].s;
@@ -442,11 +448,43 @@ int gsr_backward_multiview(int B, const gsr_view_state* views, const gsr_inputs*
     }
     {
         StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);
-        launch_gaussian_backward_multiview(P, s0->D, s0->M, s0->scale_modifier, *in, a, *grads,
-                                           reinterpret_cast<float4*>(in->shs ? aligned_base(mv_scratch) : nullptr),
-                                           st);
+        float* shx = defer ? sh_rows : reinterpret_cast<float*>(in->shs ? aligned_base(mv_scratch) : nullptr);
+        launch_gaussian_backward_multiview(P, s0->D, s0->M, s0->scale_modifier, *in, a, *grads, shx, defer, st);
     }
     GSR_STAGE("gaussian backward (multiview)");
+    return 0;
+}
+}  // namespace
+
+int gsr_backward_multiview(int B, const gsr_view_state* views, const gsr_inputs* in, void* mv_scratch,
+                           const gsr_grads* grads, void* stream) {
+    return backward_multiview_impl(B, views, in, mv_scratch, nullptr, grads, stream);
+}
+
+int gsr_backward_multiview_deferred_sh(int B, const gsr_view_state* views, const gsr_inputs* in, float* sh_rows,
+                                       const gsr_grads* grads, void* stream) {
+    if (!sh_rows) {
+        g_last_error = "[gsr] deferred SH backward: sh_rows is NULL";
+        return 1;
+    }
+    return backward_multiview_impl(B, views, in, nullptr, sh_rows, grads, stream);
+}
+
+int gsr_sh_backward(int V, int P, int D, int M, const float* shs, const float* means3D, const float* sh_rows,
+                    float* dsh, float* dmeans3D, void* stream) {
+    using namespace gsr;
+    g_last_error.clear();
+    if (V < 0 || P < 0 || D < 0 || D > 3 || M < 1 || M < (D + 1) * (D + 1))
+        return fail("[gsr] sh backward: bad V / P / D / M");
+    if (P == 0) return 0;
+    if (!shs || !means3D || (V > 0 && !sh_rows)) return fail("[gsr] sh backward: null argument");
+    if (V == 0) {
+        if (dsh) (void)hipMemsetAsync(dsh, 0, (size_t)P * M * 3 * 4, (hipStream_t)stream);
+        return 0;
+    }
+    launch_sh_backward(P, D, M, shs, means3D, V, sh_rows, dsh, dmeans3D, (hipStream_t)stream);
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return fail(std::string("[gsr] sh backward: ") + hipGetErrorString(e));
     return 0;
 }
 

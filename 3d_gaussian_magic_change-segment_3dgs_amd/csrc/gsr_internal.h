@@ -186,8 +186,15 @@ struct MvArgs {
     int B;
     MvView v[GSR_MAX_VIEWS];
 };
+// SH exchange rows of one view (gsr_sh_rows_floats): the view's clamped colour
+// gradient dRGB [P,3], then its camera centre (4 floats) at a 64-float boundary.
+__host__ __device__ inline size_t sh_rows_campos(int P) { return ((size_t)3 * P + 63) & ~(size_t)63; }
+__host__ __device__ inline size_t sh_rows_floats(int P) { return sh_rows_campos(P) + 64; }
 void launch_gaussian_backward_multiview(int P, int D, int M, float scale_modifier, const gsr_inputs& in,
-                                        const MvArgs& a, const gsr_grads& g, float4* drgb, hipStream_t st);
+                                        const MvArgs& a, const gsr_grads& g, float* shx, bool defer_sh,
+                                        hipStream_t st);
+void launch_sh_backward(int P, int D, int M, const float* shs, const float* means3D, int V, const float* shx,
+                        float* dsh, float* dmeans3D, hipStream_t st);
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
                               const float* contrib, const uint32_t* written, const float4* rec,

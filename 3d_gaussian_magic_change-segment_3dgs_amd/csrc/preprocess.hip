@@ -681,8 +681,14 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
 //    term into dmeans3D.
 // The shared inputs are read and the parameter gradients written once per batch.
 __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, float scale_modifier, gsr_inputs in,
-                                                              MvArgs a, gsr_grads g, float4* __restrict__ drgb) {
+                                                              MvArgs a, gsr_grads g, float* __restrict__ shx) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    const size_t chunk = sh_rows_floats(P);
+    if (shx && idx < a.B) {  // each view's camera centre travels with its dRGB rows
+        float* c = shx + (size_t)idx * chunk + sh_rows_campos(P);
+        const float* cp = a.v[idx].campos;
+        c[0] = cp[0]; c[1] = cp[1]; c[2] = cp[2]; c[3] = 0.f;
+    }
     if (idx >= P) return;
     const size_t i3 = 3 * (size_t)idx;
     const f3 mean = ld3(in.means3D + i3);
@@ -704,10 +710,10 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, floa
     float dop = 0.f, dseg0 = 0.f, dseg1 = 0.f;
     for (int v = 0; v < a.B; ++v) {  // uniform: the view's fields are scalar loads
         const MvView& w = a.v[v];
-        float4* drgb_v = drgb ? drgb + (size_t)v * P : nullptr;
+        float* drgb_v = shx ? shx + (size_t)v * chunk + i3 : nullptr;
         if (!(w.radii[idx] > 0)) {
             if (w.dmeans2D) { w.dmeans2D[i3] = 0.f; w.dmeans2D[i3 + 1] = 0.f; w.dmeans2D[i3 + 2] = 0.f; }
-            if (drgb_v) drgb_v[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (drgb_v) { drgb_v[0] = 0.f; drgb_v[1] = 0.f; drgb_v[2] = 0.f; }
             continue;
         }
         const float4 r0 = w.rec[(size_t)idx * REC_F4], r1 = w.rec[(size_t)idx * REC_F4 + 1];
@@ -741,8 +747,9 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, floa
         dseg1 += q[4];
         if (drgb_v) {
             const uint8_t cbits = w.clamped[idx];
-            drgb_v[idx] = make_float4((cbits & 1) ? 0.f : q[0], (cbits & 2) ? 0.f : q[1], (cbits & 4) ? 0.f : q[2],
-                                      0.f);
+            drgb_v[0] = (cbits & 1) ? 0.f : q[0];
+            drgb_v[1] = (cbits & 2) ? 0.f : q[1];
+            drgb_v[2] = (cbits & 4) ? 0.f : q[2];
         }
         const float* view = w.view;
         const float* proj = w.proj;
@@ -886,10 +893,11 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, floa
 // read / written per thread.
 template <bool STAGED>
 __global__ void __launch_bounds__(256) k_gaussian_backward_mv_sh(int P, int D, int M, const float* __restrict__ shs,
-                                                                 const float* __restrict__ means3D, MvArgs a,
-                                                                 const float4* __restrict__ drgb,
+                                                                 const float* __restrict__ means3D, int V,
+                                                                 const float* __restrict__ shx,
                                                                  float* __restrict__ dsh,
                                                                  float* __restrict__ dmeans3D) {
+    const size_t chunk = sh_rows_floats(P);
     __shared__ float rows[STAGED ? 4 : 1][STAGED ? 64 : 1][52];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wbase = blockIdx.x * blockDim.x + wave * 64;
@@ -919,11 +927,11 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv_sh(int P, int D, i
     for (int i = 0; i < 48; ++i) acc[i] = 0.f;
     f3 dn_sum = {0.f, 0.f, 0.f};
     const f3 mean = live ? ld3(means3D + 3 * (size_t)idx) : f3{0.f, 0.f, 0.f};
-    for (int v = 0; v < a.B; ++v) {
-        const float4 c = live ? drgb[(size_t)v * P + idx] : make_float4(0.f, 0.f, 0.f, 0.f);
-        if (c.x == 0.f && c.y == 0.f && c.z == 0.f) continue;  // invisible in this view (or a zero gradient)
-        const f3 dRGB = {c.x, c.y, c.z};
-        const f3 dir_orig = mean - ld3(a.v[v].campos);
+    for (int v = 0; v < V; ++v) {  // views in order: every rank of an exchange sums identically
+        const float* rows = shx + (size_t)v * chunk;
+        const f3 dRGB = live ? ld3(rows + 3 * (size_t)idx) : f3{0.f, 0.f, 0.f};
+        if (dRGB.x == 0.f && dRGB.y == 0.f && dRGB.z == 0.f) continue;  // invisible in this view (or a zero gradient)
+        const f3 dir_orig = mean - ld3(rows + sh_rows_campos(P));
         const f3 dir = dir_orig / sqrtf(dot3(dir_orig, dir_orig));
         float bas[16];
 #pragma unroll
@@ -1031,20 +1039,27 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 }
 
 void launch_gaussian_backward_multiview(int P, int D, int M, float scale_modifier, const gsr_inputs& in,
-                                        const MvArgs& a, const gsr_grads& g, float4* drgb, hipStream_t st) {
+                                        const MvArgs& a, const gsr_grads& g, float* shx, bool defer_sh,
+                                        hipStream_t st) {
     if (P == 0) return;
-    float4* drgb_used = (in.shs && (g.dsh || g.dmeans3D)) ? drgb : nullptr;
-    hipLaunchKernelGGL(k_gaussian_backward_mv, dim3(cdiv(P, 256)), dim3(256), 0, st, P, M, scale_modifier, in, a, g,
-                       drgb_used);
-    if (!drgb_used) return;
-    const bool staged = M == 16 && (reinterpret_cast<uintptr_t>(in.shs) & 15) == 0 &&
-                        (!g.dsh || (reinterpret_cast<uintptr_t>(g.dsh) & 15) == 0);
+    float* shx_used = (in.shs && (defer_sh || g.dsh || g.dmeans3D)) ? shx : nullptr;
+    hipLaunchKernelGGL(k_gaussian_backward_mv, dim3(cdiv(P, 256)), dim3(256),
+                       0, st, P, M, scale_modifier, in, a, g, shx_used);
+    if (!shx_used || defer_sh) return;
+    launch_sh_backward(P, D, M, in.shs, in.means3D, a.B, shx_used, g.dsh, g.dmeans3D, st);
+}
+
+void launch_sh_backward(int P, int D, int M, const float* shs, const float* means3D, int V, const float* shx,
+                        float* dsh, float* dmeans3D, hipStream_t st) {
+    if (P == 0 || V == 0) return;
+    const bool staged = M == 16 && (reinterpret_cast<uintptr_t>(shs) & 15) == 0 &&
+                        (!dsh || (reinterpret_cast<uintptr_t>(dsh) & 15) == 0);
     if (staged)
-        hipLaunchKernelGGL(k_gaussian_backward_mv_sh<true>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, in.shs,
-                           in.means3D, a, drgb_used, g.dsh, g.dmeans3D);
+        hipLaunchKernelGGL(k_gaussian_backward_mv_sh<true>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, shs,
+                           means3D, V, shx, dsh, dmeans3D);
     else
-        hipLaunchKernelGGL(k_gaussian_backward_mv_sh<false>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, in.shs,
-                           in.means3D, a, drgb_used, g.dsh, g.dmeans3D);
+        hipLaunchKernelGGL(k_gaussian_backward_mv_sh<false>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, shs,
+                           means3D, V, shx, dsh, dmeans3D);
 }
 
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,

@@ -86,6 +86,14 @@ _lib.gsr_backward_multiview.restype = _i
 _lib.gsr_backward_multiview.argtypes = [_i, ctypes.POINTER(_ViewState), ctypes.POINTER(_Inputs), _vp,
                                         ctypes.POINTER(_Grads), _vp]
 
+_lib.gsr_sh_rows_floats.restype = _sz
+_lib.gsr_sh_rows_floats.argtypes = [_i]
+_lib.gsr_backward_multiview_deferred_sh.restype = _i
+_lib.gsr_backward_multiview_deferred_sh.argtypes = [_i, ctypes.POINTER(_ViewState), ctypes.POINTER(_Inputs), _vp,
+                                                    ctypes.POINTER(_Grads), _vp]
+_lib.gsr_sh_backward.restype = _i
+_lib.gsr_sh_backward.argtypes = [_i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]
+
 _ll = ctypes.c_longlong
 _lib.gsr_arena_layout.restype = _ll
 _lib.gsr_arena_layout.argtypes = [_i, _i, _i, ctypes.POINTER(_ll)]
@@ -104,7 +112,8 @@ EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_img_bytes", "gsr
                     "gsr_forward_geometry", "gsr_forward_render", "gsr_backward", "gsr_mark_visible",
                     "gsr_debug_copy", "gsr_num_stages", "gsr_stage_name", "gsr_timing_enable", "gsr_timing_collect",
                     "gsr_last_error", "gsr_version", "gsr_set_option", "gsr_multiview_scratch_bytes",
-                    "gsr_backward_multiview")
+                    "gsr_backward_multiview", "gsr_sh_rows_floats", "gsr_backward_multiview_deferred_sh",
+                    "gsr_sh_backward")
 
 _DEBUG_FIELDS = {  # name -> (dtype, elements per unit, unit: P | I | T)
     "tiles_touched": (torch.int32, 1, "P"), "rec": (torch.float32, 16, "P"), "clamped": (torch.uint8, 1, "P"),
@@ -368,8 +377,30 @@ def mark_visible(means3D, viewmatrix, projmatrix):
     return present
 
 
+def sh_rows_floats(P):
+    """Floats of one view's SH exchange rows (include/gsr.h gsr_sh_rows_floats)."""
+    return int(_lib.gsr_sh_rows_floats(int(P)))
+
+
+def sh_backward(sh_rows, V, means3D, sh, degree, dsh, dmeans3D):
+    """gsr_sh_backward: from V views' SH exchange rows (sh_rows: fp32, V x
+    sh_rows_floats(P), on the GPU), write dsh [P,M,3] = sum over the views of
+    basis x dRGB and add the SH direction term of every view to dmeans3D [P,3]."""
+    P = int(means3D.size(0))
+    M = int(sh.size(1))
+    device = means3D.device
+    for t, n in ((sh_rows, "sh_rows"), (means3D, "means3D"), (sh, "sh"), (dsh, "dsh"), (dmeans3D, "dmeans3D")):
+        if t is not None and (t.device != device or t.dtype != torch.float32 or not t.is_contiguous()):
+            raise RuntimeError(f"sh_backward: {n} must be a contiguous float32 tensor on {device}")
+    if sh_rows.numel() < int(V) * sh_rows_floats(P):
+        raise RuntimeError("sh_backward: sh_rows holds fewer than V views")
+    with torch.cuda.device(device):
+        _check(_lib.gsr_sh_backward(int(V), P, int(degree), M, sh.data_ptr(), means3D.data_ptr(),
+                                    sh_rows.data_ptr(), _ptr(dsh), _ptr(dmeans3D), _stream(device)))
+
+
 def rasterize_gaussians_backward_multiview(views, means3D, colors, segments, scales, rotations, scale_modifier,
-                                           cov3D_precomp, sh, degree, debug):
+                                           cov3D_precomp, sh, degree, debug, sh_rows=None):
     """gsr_backward_multiview: the summed parameter gradients of several views.
     `views` holds, per view, the raster settings fields (bg, viewmatrix, projmatrix,
     tanfovx, tanfovy, image_height, image_width, campos), the forward state
@@ -377,7 +408,12 @@ def rasterize_gaussians_backward_multiview(views, means3D, colors, segments, sca
     (dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha; None = zeros).  Returns the
     single-view tuple (dmeans2D = None, dcolors, dopacity, dmeans3D, dcov3D, dsh,
     dscales, drot, dsegments) -- one gradient arena, bucket first -- and the list of
-    per-view dmeans2D [P,3]."""
+    per-view dmeans2D [P,3].
+
+    sh_rows (fp32 tensor of B x sh_rows_floats(P) on the GPU, 16-B aligned): deferred
+    SH mode (gsr_backward_multiview_deferred_sh) -- the views' SH exchange rows are
+    written there, dsh is left unwritten and dmeans3D lacks the SH direction term
+    until sh_backward completes them (after a view-parallel exchange)."""
     B = len(views)
     if not 1 <= B <= MAX_VIEWS:
         raise RuntimeError(f"multiview backward: 1..{MAX_VIEWS} views per call")
@@ -438,7 +474,8 @@ def rasterize_gaussians_backward_multiview(views, means3D, colors, segments, sca
             S.scratch = scratch.data_ptr() if R > 0 else None
             S.dmeans2D = d2[v].data_ptr()
         inp = _inputs(means3D_, sh_, colors_, segments_, None, scales_, rotations_, cov_)
-        mv = torch.empty(_lib.gsr_multiview_scratch_bytes(P, B), dtype=torch.uint8, device=device)
+        mv = torch.empty(_lib.gsr_multiview_scratch_bytes(P, B) if sh_rows is None else 1, dtype=torch.uint8,
+                         device=device)
         g = _Grads()
         g.dmeans2D, g.dopacity, g.dmeans3D = None, dopacity.data_ptr(), dmeans3D.data_ptr()
         g.dcolors = dcolors.data_ptr() if colors_ is not None else None
@@ -447,6 +484,16 @@ def rasterize_gaussians_backward_multiview(views, means3D, colors, segments, sca
         g.dscales = dscales.data_ptr() if scales_ is not None else None
         g.drot = drot.data_ptr() if scales_ is not None else None
         g.dsegments = dsegments.data_ptr()
-        _check(_lib.gsr_backward_multiview(B, states, ctypes.byref(inp), mv.data_ptr(), ctypes.byref(g),
-                                           _stream(device)))
+        if sh_rows is not None:
+            if sh_ is None:
+                raise RuntimeError("deferred SH backward needs SH coefficients (shs)")
+            if (sh_rows.device != device or sh_rows.dtype != torch.float32 or not sh_rows.is_contiguous()
+                    or sh_rows.numel() < B * sh_rows_floats(P) or sh_rows.data_ptr() % 16):
+                raise RuntimeError("sh_rows must be a contiguous, 16-B aligned float32 GPU tensor of "
+                                   "B x sh_rows_floats(P) floats")
+            _check(_lib.gsr_backward_multiview_deferred_sh(B, states, ctypes.byref(inp), sh_rows.data_ptr(),
+                                                           ctypes.byref(g), _stream(device)))
+        else:
+            _check(_lib.gsr_backward_multiview(B, states, ctypes.byref(inp), mv.data_ptr(), ctypes.byref(g),
+                                               _stream(device)))
     return out, d2

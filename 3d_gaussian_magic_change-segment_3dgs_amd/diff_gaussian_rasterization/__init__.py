@@ -7,6 +7,7 @@ GaussianRasterizer with forward/markVisible (:182-235), rasterize_gaussians
 gaussian_renderer/__init__.py imports and calls it unchanged.  The compute path
 is libgsr.so (hand-written HIP for gfx950) through the ctypes module `_C`.
 """
+import threading
 from typing import NamedTuple
 
 import torch
@@ -15,7 +16,54 @@ import torch.nn as nn
 from . import _C
 
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
-           "rasterize_gaussians_multiview"]
+           "rasterize_gaussians_multiview", "defer_sh_gradients"]
+
+_tls = threading.local()
+
+
+class defer_sh_gradients:
+    """Context manager for view-parallel training (gsr_tools.dp.ShExchange): backward
+    passes run inside it leave the SH gradient to a later exchange.  They write
+    each view's SH exchange rows (include/gsr.h gsr_backward_multiview_deferred_sh)
+    to a buffer obtained from `sink.sh_rows(B, P, device)` and report the call with
+    `sink.record(...)`; the returned dsh is NOT written yet and dmeans3D lacks the
+    SH direction term until the sink runs _C.sh_backward.  Calls without SH
+    coefficients (colors_precomp) are unaffected.  An extension of the reference API."""
+
+    def __init__(self, sink):
+        self.sink = sink
+
+    def __enter__(self):
+        stack = getattr(_tls, "sinks", None)
+        if stack is None:
+            stack = _tls.sinks = []
+        stack.append(self.sink)
+        return self.sink
+
+    def __exit__(self, *exc):
+        _tls.sinks.pop()
+        return False
+
+
+def _sh_sink():
+    stack = getattr(_tls, "sinks", None)
+    return stack[-1] if stack else None
+
+
+def _backward_views(views, means3D, colors_precomp, segments, scales, rotations, scale_modifier, cov3Ds_precomp,
+                    sh, sh_degree, debug):
+    """Multi-view backward, deferred-SH when a defer_sh_gradients sink is active."""
+    sink = _sh_sink()
+    rows = None
+    if sink is not None and isinstance(sh, torch.Tensor) and sh.numel() > 0:
+        rows = sink.sh_rows(len(views), int(means3D.size(0)), means3D.device)
+    out, d2 = _C.rasterize_gaussians_backward_multiview(views, means3D, colors_precomp, segments, scales, rotations,
+                                                        scale_modifier, cov3Ds_precomp, sh, sh_degree, debug,
+                                                        sh_rows=rows)
+    if rows is not None:
+        _, _, _, g_means3D, _, g_sh, _, _, _ = out
+        sink.record(rows, len(views), means3D, sh, sh_degree, g_sh, g_means3D)
+    return out, d2
 
 
 def cpu_deep_copy_tuple(input_tuple):
@@ -130,7 +178,18 @@ class _RasterizeGaussians(torch.autograd.Function):
                 imgBuffer,
                 alpha,
                 raster_settings.debug)
-        if raster_settings.debug:
+        if _sh_sink() is not None and sh.numel() > 0:
+            rs = raster_settings
+            view = {"bg": rs.bg, "viewmatrix": rs.viewmatrix, "projmatrix": rs.projmatrix, "tanfovx": rs.tanfovx,
+                    "tanfovy": rs.tanfovy, "image_height": rs.image_height, "image_width": rs.image_width,
+                    "campos": rs.campos, "radii": radii, "geom": geomBuffer, "binning": binningBuffer,
+                    "img": imgBuffer, "num_rendered": num_rendered, "alpha": alpha, "dL_dcolor": grad_color,
+                    "dL_dsegment": grad_segment, "dL_ddepth": grad_depth, "dL_dalpha": grad_alpha}
+            (_, g_col, g_op, g_m3, g_cov, g_sh, g_sc, g_rot, g_seg), d2 = _backward_views(
+                [view], means3D, colors_precomp, segments, scales, rotations, rs.scale_modifier, cov3Ds_precomp, sh,
+                rs.sh_degree, rs.debug)
+            out = (d2[0], g_col, g_op, g_m3, g_cov, g_sh, g_sc, g_rot, g_seg)
+        elif raster_settings.debug:
             cpu_args = cpu_deep_copy_tuple(args)
             try:
                 out = _C.rasterize_gaussians_backward(*args)
@@ -210,9 +269,8 @@ class _RasterizeGaussiansMultiview(torch.autograd.Function):
                           "binning": binning, "img": img, "num_rendered": num_rendered, "alpha": alpha,
                           "dL_dcolor": gc, "dL_dsegment": gs, "dL_ddepth": gd, "dL_dalpha": ga})
         (_, g_colors, g_opacities, g_means3D, g_cov3D, g_sh, g_scales, g_rot, g_segments), d2 = \
-            _C.rasterize_gaussians_backward_multiview(views, means3D, colors_precomp, segments, scales, rotations,
-                                                      rs0.scale_modifier, cov3Ds_precomp, sh, rs0.sh_degree,
-                                                      rs0.debug)
+            _backward_views(views, means3D, colors_precomp, segments, scales, rotations, rs0.scale_modifier,
+                            cov3Ds_precomp, sh, rs0.sh_degree, rs0.debug)
         ctx.views = None
         return (g_means3D, g_sh, g_colors, g_segments, g_opacities, g_scales, g_rot, g_cov3D, None, *d2)
 

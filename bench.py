@@ -29,6 +29,7 @@ Prints ONE JSON line on rank 0.  Extra objects:
                   same workload (whole views, rank 0, N = 1 only).
 """
 import argparse
+import contextlib
 import json
 import math
 import os
@@ -46,6 +47,14 @@ import torch  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 SIMD_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1_pmc_summary.json")
+
+
+EXCHANGE_DESC = {
+    "allreduce": "one RCCL all-reduce of the 61 f32/Gaussian grad bucket",
+    "sh": "SH exchange: RCCL all-gather of each view's 3-float dRGB rows + all-reduce of the 13 non-SH "
+          "f32/Gaussian, dsh rebuilt on every rank (gsr_tools.dp.ShExchange)",
+    None: "",
+}
 
 
 def algorithmic_bytes(stage, P, I, HW, deg, views=1):
@@ -114,6 +123,10 @@ def main():
                          "iteration at N GPUs; >1: one multi-view backward and one all-reduce per step)")
     ap.add_argument("--batched-views", type=int, default=8,
                     help="also time steps of this many views per rank (reported under 'batched'; 1 = skip)")
+    ap.add_argument("--exchange", choices=["auto", "allreduce", "sh"], default="auto",
+                    help="N>1 gradient exchange: one all-reduce of the 61-float bucket, or the SH exchange "
+                         "(all-gather of 3-float dRGB rows + all-reduce of 13 floats, gsr_tools.dp.ShExchange); "
+                         "auto = the one with fewer bytes per link for the step's views per rank")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -170,15 +183,23 @@ def main():
 
     pending = []  # the exchange in flight: (work handle, gradients kept alive)
 
-    def exchange(g):
-        # One RCCL all-reduce of the gradient bucket per step, on RCCL's stream: it runs
-        # while the next step renders (the metric excludes the optimizer step, so no
-        # later work waits for it); at most one exchange is in flight.
+    def exchange_kind(nv):
+        if dist is None:
+            return None
+        return dp.choose_exchange(world, nv, shs.shape[1]) if args.exchange == "auto" else args.exchange
+
+    def exchange(g, ex=None):
+        # One exchange per step, on RCCL's stream (+ the SH completion on a side stream
+        # for ShExchange): it runs while the next step renders (the metric excludes the
+        # optimizer step, so no later work waits for it); at most one is in flight.
         if dist is None:
             return
         while pending:
             pending.pop()[0].wait()
-        h = dist.all_reduce(dp.bucket(dp.arena_of(g[0]), P, shs.shape[1]), op=dist.ReduceOp.SUM, async_op=True)
+        if ex is not None:
+            h = ex.start()
+        else:
+            h = dist.all_reduce(dp.bucket(dp.arena_of(g[0]), P, shs.shape[1]), op=dist.ReduceOp.SUM, async_op=True)
         pending.append((h, g))
 
     def drain():
@@ -186,7 +207,16 @@ def main():
             pending.pop()[0].wait()
 
     def make_step(nv):
+        kind = exchange_kind(nv)
+
         def step():
+            ex = dp.ShExchange() if kind == "sh" else None
+            with dgr.defer_sh_gradients(ex) if ex is not None else contextlib.nullcontext():
+                g = grads_of_views()
+            exchange(g, ex)
+            return g
+
+        def grads_of_views():
             if nv == 1:
                 # one view through the drop-in API (GaussianRasterizer's autograd function)
                 color, radii, depth, alpha, segment = dgr.rasterize_gaussians(means3D, means2D[0], shs, E, segs,
@@ -201,8 +231,8 @@ def main():
                 state["I"] = sum(v[0] for v in outs[0][0].grad_fn.views) / nv
                 g = torch.autograd.grad([t for o in outs for t in (o[0], o[2], o[3], o[4])],
                                         params + means2D[:nv], up_list * nv)
-            exchange(g)
             return g
+        step.exchange = kind
         return step
 
     step = make_step(B)
@@ -297,9 +327,9 @@ def main():
                                f"rank per step" + (" (per-view forward, one multi-view backward)" if B > 1 else
                                                    " through the drop-in GaussianRasterizer"), "P": P, "width": W, "height": H, "sh_degree": deg,
                    "num_classes": 2, "num_rendered": I, "global_batch": world * B, "views_per_step_per_gpu": B,
-                   "parallelism": f"dp{world}" + (" (views sharded; one RCCL all-reduce of the 61 f32/Gaussian "
-                                                  "grad bucket per step, overlapped with the next step's "
-                                                  "render)" if world > 1 else "")},
+                   "parallelism": f"dp{world}" + ((" (views sharded; " + EXCHANGE_DESC[step.exchange] +
+                                                   " per step, overlapped with the next step's render)")
+                                                  if world > 1 else "")},
         "roofline": roof,
         "stages": stages,
     }
@@ -317,7 +347,8 @@ def main():
         out["batched"] = {"views_per_step_per_gpu": BB, "global_batch": world * BB, "steps": k,
                           "value": round(world * BB * k / el_b, 2), "unit": "views/s",
                           "ms_per_step": round(1e3 * el_b / k, 4),
-                          "note": "per-view forward + one gsr_backward_multiview over the batch + one all-reduce"}
+                          "exchange": bstep.exchange,
+                          "note": "per-view forward + one gsr_backward_multiview over the batch + one exchange"}
     out["train_step"] = None
     if rank == 0 and world == 1 and not args.no_train:
         from gsr_tools import train_bench

@@ -157,6 +157,33 @@ typedef struct gsr_view_state {
 GSR_API size_t gsr_multiview_scratch_bytes(int P, int B);
 GSR_API int gsr_backward_multiview(int B, const gsr_view_state* views, const gsr_inputs* in, void* mv_scratch,
                                    const gsr_grads* grads, void* stream);
+/* ---- view-parallel exchange of the SH gradient.  For one view
+ * the SH-coefficient gradient is the outer product basis(dir) x dRGB
+ * (backward.cu:46-110): 48 floats per Gaussian determined by 3 (the clamped
+ * colour gradient) and the camera centre.  A data-parallel trainer therefore
+ * exchanges each view's dRGB rows (all-gather, 12 B per Gaussian and view) instead
+ * of all-reducing dsh (192 B per Gaussian), and every rank rebuilds the summed dsh
+ * and the SH direction term of dmeans3D locally with gsr_sh_backward.
+ *
+ * gsr_sh_rows_floats(P): floats of one view's rows: dRGB [P,3], then the view's
+ * camera centre (x, y, z, 0) at float offset roundup(3P, 64).
+ *
+ * gsr_backward_multiview_deferred_sh: gsr_backward_multiview (shs required) that
+ * writes the B views' rows to sh_rows [B][gsr_sh_rows_floats(P)] (16-B aligned)
+ * and leaves grads->dsh unwritten and grads->dmeans3D WITHOUT the SH direction
+ * term; all other gradients are complete (summed over the B views).
+ *
+ * gsr_sh_backward: for V views' rows (in order; every rank sums in the same order,
+ * so all ranks get identical bits), writes dsh [P,M,3] = sum_v basis_v x dRGB_v
+ * (coefficients >= (D+1)^2 written as 0) and ADDS the SH direction term of every
+ * view to dmeans3D [P,3] (either may be NULL).  Run after the non-SH gradients are
+ * all-reduced, the result equals the all-reduce of the complete gradients. */
+GSR_API size_t gsr_sh_rows_floats(int P);
+GSR_API int gsr_backward_multiview_deferred_sh(int B, const gsr_view_state* views, const gsr_inputs* in,
+                                               float* sh_rows, const gsr_grads* grads, void* stream);
+GSR_API int gsr_sh_backward(int V, int P, int D, int M, const float* shs, const float* means3D,
+                            const float* sh_rows, float* dsh, float* dmeans3D, void* stream);
+
 /* ---- frustum visibility: present[i] = (view-space z > 0.2).  Replaces
  * markVisible (rasterize_points.cu:223-242, rasterizer_impl.cu:54-66). */
 GSR_API int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

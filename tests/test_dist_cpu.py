@@ -109,3 +109,118 @@ def test_densification_stats_reduction_gloo_ws2():
     for rank, a, d, r in res:
         np.testing.assert_allclose(a, ref[0].numpy(), rtol=1e-6)
         assert np.array_equal(d, ref[1].numpy()) and np.array_equal(r, ref[2].numpy())
+
+
+# ---- ShExchange: gathered dRGB rows + all-reduce of the non-SH blocks ----------
+C0 = 0.28209479177387814  # auxiliary.h:21
+
+
+def _sh_terms_f64(means3D, shs, deg, campos, drgb):
+    """fp64 restatement (test-only) of one view's SH gradient terms: dsh = basis x dRGB
+    (backward.cu:46-110) and the direction term of dmeans3D (the true derivative of
+    dRGB . colour(dir(mean)), which the reference's hand formula computes)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from test_oracle_autograd import sh_basis
+    K = (deg + 1) ** 2
+    m = means3D.double().clone().requires_grad_(True)
+    d = m - campos.double()
+    d = d / d.norm(dim=1, keepdim=True)
+    bas = sh_basis(deg, d)  # [P, K]
+    col = (bas[:, :, None] * shs.double()[:, :K, :]).sum(1)
+    (dn,) = torch.autograd.grad((col * drgb.double()).sum(), m)
+    dsh = torch.zeros(shs.shape, dtype=torch.float64)
+    dsh[:, :K, :] = bas.detach()[:, :, None] * drgb.double()[:, None, :]
+    return dsh, dn
+
+
+def _sh_backward_f64(rows_all, V, means3D, sh, degree, dsh, dmeans3D):
+    """Stand-in for _C.sh_backward on CPU tensors (reads the same row layout)."""
+    from diff_gaussian_rasterization._C import sh_rows_floats
+    P = means3D.shape[0]
+    ch = sh_rows_floats(P)
+    cpos = ch - 64
+    acc_sh = torch.zeros(sh.shape, dtype=torch.float64)
+    acc_dn = torch.zeros(P, 3, dtype=torch.float64)
+    for v in range(V):
+        r = rows_all[v * ch:(v + 1) * ch]
+        a, b = _sh_terms_f64(means3D, sh, degree, r[cpos:cpos + 3], r[:3 * P].view(P, 3))
+        acc_sh += a
+        acc_dn += b
+    dsh.copy_(acc_sh.float())
+    dmeans3D.add_(acc_dn.float())
+
+
+def _sh_scene():
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd")]
+    from gsr_tools.scene import synthetic_scene, orbit_camera
+    return synthetic_scene(P_TEST, sh_degree=3, seed=31), [orbit_camera(v, 96, 64, 80.0, n_views=8) for v in range(2)]
+
+
+def _sh_worker(rank, world, port, out_q):
+    import sys
+    sys.path[:0] = [ROOT, os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd")]
+    from gsr_tools import dp
+    from diff_gaussian_rasterization._C import sh_rows_floats
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    scene, cams = _sh_scene()
+    g, M = _per_view_grads(rank)
+    # deferred form of this view's gradients: dRGB rows + dmeans3D without the SH
+    # direction term, dsh left as garbage (the exchange must overwrite all of it)
+    drgb = torch.from_numpy(g["dsh"][:, 0, :]).float() / C0
+    campos = cams[rank].camera_center.float()
+    _, dn = _sh_terms_f64(scene.means3D, scene.shs, 3, campos, drgb)
+    g = dict(g)
+    g["dmeans3D"] = (torch.from_numpy(g["dmeans3D"]).double() - dn).float().numpy()
+    g["dsh"] = np.full_like(g["dsh"], np.nan)
+    arena = dp.pack_arena(g, P_TEST, M)
+    lay = dp.arena_layout(P_TEST, M)
+    dmeans3D = arena.narrow(0, lay["dmeans3D"][0], 3 * P_TEST).view(P_TEST, 3)
+    dsh = arena.narrow(0, lay["dsh"][0], 3 * M * P_TEST).view(P_TEST, M, 3)
+    ex = dp.ShExchange(sh_backward=_sh_backward_f64)
+    rows = ex.sh_rows(1, P_TEST, torch.device("cpu"))
+    rows.zero_()
+    rows[:3 * P_TEST] = drgb.reshape(-1)
+    rows[sh_rows_floats(P_TEST) - 64:sh_rows_floats(P_TEST) - 61] = campos
+    ex.record(rows, 1, scene.means3D.float(), scene.shs.float(), 3, dsh, dmeans3D)
+    ex.start().wait()
+    out_q.put((rank, dp.bucket(arena, P_TEST, M).numpy().copy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_sh_exchange_gloo_ws2():
+    """ShExchange's bucket equals the all-reduce of the complete per-view gradients."""
+    from gsr_tools import dp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sh_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    ref = None
+    for view in range(2):
+        g, M = _per_view_grads(view)
+        bk = dp.bucket(dp.pack_arena(g, P_TEST, M), P_TEST, M).numpy()
+        ref = bk if ref is None else ref + bk
+    lay = dp.arena_layout(P_TEST, M)
+    (r0, b0), (r1, b1) = sorted(res, key=lambda t: t[0])
+    assert np.array_equal(b0, b1), "every rank must hold the same bits"
+    for name in ("dmeans3D", "dsh", "dopacity", "dscales", "drot", "dsegments"):
+        o, k = lay[name]
+        a, r = b0[o:o + k * P_TEST], ref[o:o + k * P_TEST]
+        err = np.abs(a.astype(np.float64) - r).max() / max(np.abs(r).max(), 1e-30)
+        assert err < 2e-6, (name, err)
+
+
+def test_exchange_choice():
+    from gsr_tools import dp
+    assert dp.choose_exchange(2, 1) == "sh" and dp.choose_exchange(8, 1) == "sh"
+    assert dp.choose_exchange(8, 8) == "allreduce"
+    c = dp.exchange_bytes(2, 1)
+    assert c["allreduce"] / c["sh_exchange"] > 3.5

@@ -128,3 +128,106 @@ def test_multiview_view_with_nothing_visible(gpu_available):
     far = orbit_camera(0, 160, 120, 150.0, radius=-4.0)  # camera behind the scene, looking away
     views.append((Hn.settings_for(far, 3, DEV), Hn.upstream_grads(120, 160, seed=99)))
     _check(d, views)
+
+
+# ---- deferred SH gradients (include/gsr.h gsr_backward_multiview_deferred_sh +
+# gsr_sh_backward): the split into "rows now, SH later" runs the same per-Gaussian
+# arithmetic in the same order, so the completed gradients are bit-identical.
+class _Sink:
+    def __init__(self):
+        self.entries = []
+
+    def sh_rows(self, B, P, device):
+        from diff_gaussian_rasterization import _C
+        return torch.full((B * _C.sh_rows_floats(P),), float("nan"), dtype=torch.float32, device=device)
+
+    def record(self, rows, B, means3D, sh, degree, dsh, dmeans3D):
+        self.entries.append((rows, B, means3D, sh, degree, dsh, dmeans3D))
+
+
+@pytest.mark.parametrize("n_views,deg,sh_take", [(1, 3, None), (3, 3, None), (3, 2, 9)])
+def test_deferred_sh_completes_to_multiview(gpu_available, n_views, deg, sh_take):
+    from diff_gaussian_rasterization import _C, defer_sh_gradients
+    scene = synthetic_scene(5000, sh_degree=3, seed=47)
+    d = _leaves(scene, sh_take=sh_take)
+    views = _views(n_views, deg)
+    ref, ref_d2, _ = _multi(d, views)
+    sink = _Sink()
+    with defer_sh_gradients(sink):
+        got, got_d2, _ = _multi(d, views)
+    assert len(sink.entries) == 1
+    rows, B, means3D, sh, degree, dsh, dmeans3D = sink.entries[0]
+    assert B == n_views and dsh.data_ptr() == got["shs"].data_ptr()
+    P = scene.P
+    ch = _C.sh_rows_floats(P)
+    for v, (st, _) in enumerate(views):  # each view's camera centre travels with its rows
+        assert torch.equal(rows[v * ch + ch - 64:v * ch + ch - 61], st.campos.float())
+    _C.sh_backward(rows, B, means3D.detach(), sh.detach(), degree, dsh, dmeans3D)
+    for k in ref:
+        assert torch.equal(got[k], ref[k]), f"{k} differs after the SH completion"
+    for a, b in zip(got_d2, ref_d2):
+        assert torch.equal(a, b)
+
+
+def test_sh_backward_two_batches_sum(gpu_available):
+    """Rows of two batches completed together equal the multi-view backward of all
+    views (what every rank computes after the all-gather)."""
+    from diff_gaussian_rasterization import _C, defer_sh_gradients
+    scene = synthetic_scene(4000, sh_degree=3, seed=48)
+    d = _leaves(scene)
+    views = _views(4, 3)
+    ref, _, _ = _multi(d, views)
+    parts = []
+    for half in (views[:2], views[2:]):
+        sink = _Sink()
+        with defer_sh_gradients(sink):
+            g, _, _ = _multi(d, half)
+        parts.append((g, sink.entries[0]))
+    (g0, e0), (g1, e1) = parts
+    rows_all = torch.cat([e0[0], e1[0]])
+    # the non-SH blocks are summed as an all-reduce would; then the SH completion
+    dm = (g0["means3D"] + g1["means3D"]).contiguous()
+    dsh = torch.empty_like(g0["shs"])
+    _C.sh_backward(rows_all, 4, d["means3D"].detach(), d["shs"].detach(), 3, dsh, dm)
+    for k, got in (("shs", dsh), ("means3D", dm), ("opacities", g0["opacities"] + g1["opacities"]),
+                   ("scales", g0["scales"] + g1["scales"]), ("rotations", g0["rotations"] + g1["rotations"])):
+        r = ref[k].double()
+        err = float((got.double() - r).norm() / max(float(r.norm()), 1e-30))
+        assert err <= 1e-6, f"{k}: normwise error {err:.2e}"
+
+
+def test_sh_exchange_single_rank_equals_dropin(gpu_available):
+    """gsr_tools.dp.ShExchange around the drop-in single-view backward (world size 1
+    over gloo): the exchanged bucket equals the drop-in backward's bucket."""
+    import os
+    import socket
+    import torch.distributed as dist
+    from diff_gaussian_rasterization import defer_sh_gradients
+    from gsr_tools import dp
+    scene = synthetic_scene(5000, sh_degree=3, seed=49)
+    d = _leaves(scene)
+    views = _views(1, 3)
+    ref, _ = _single(d, views)
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=0, world_size=1)
+    try:
+        from diff_gaussian_rasterization import rasterize_gaussians
+        st, ups = views[0]
+        m2 = torch.zeros_like(d["means3D"], requires_grad=True)
+        color, radii, depth, alpha, seg = rasterize_gaussians(d["means3D"], m2, raster_settings=st, **_kw(d))
+        ex = dp.ShExchange()
+        with defer_sh_gradients(ex):
+            grads = torch.autograd.grad([color, depth, alpha, seg], [d[k] for k in d],
+                                        [ups["color"].to(DEV), ups["depth"].to(DEV), ups["alpha"].to(DEV),
+                                         ups["segment"].to(DEV)])
+        assert len(ex.entries) == 1
+        ex.start().wait()  # nothing reads the deferred gradients before this
+        got = {k: g.double() for k, g in zip(d, grads)}
+    finally:
+        dist.destroy_process_group()
+    for k, r in ref.items():
+        err = float((got[k] - r).norm() / max(float(r.norm()), 1e-30))
+        assert err <= 1e-6, f"{k}: normwise error {err:.2e}"
