@@ -392,7 +392,7 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
     }
     const int P = s0->P;
     if (P == 0) return 0;
-    if (in->shs && !mv_scratch) return fail("[gsr] multiview: scratch is NULL");
+    if (in->shs && !mv_scratch && !defer) return fail("[gsr] multiview: scratch is NULL");
     hipStream_t st = (hipStream_t)stream;
     const bool dbg = s0->debug != 0;
     MvArgs a{};

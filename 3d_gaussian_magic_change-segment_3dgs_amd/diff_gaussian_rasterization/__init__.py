@@ -18,7 +18,10 @@ from . import _C
 __all__ = ["GaussianRasterizationSettings", "GaussianRasterizer", "rasterize_gaussians",
            "rasterize_gaussians_multiview", "defer_sh_gradients"]
 
-_tls = threading.local()
+# Process-wide, not thread-local: autograd runs the backward of GPU tensors on its own
+# device thread, not on the thread that entered the context.
+_SINKS = []
+_SINKS_LOCK = threading.Lock()
 
 
 class defer_sh_gradients:
@@ -28,26 +31,27 @@ class defer_sh_gradients:
     to a buffer obtained from `sink.sh_rows(B, P, device)` and report the call with
     `sink.record(...)`; the returned dsh is NOT written yet and dmeans3D lacks the
     SH direction term until the sink runs _C.sh_backward.  Calls without SH
-    coefficients (colors_precomp) are unaffected.  An extension of the reference API."""
+    coefficients (colors_precomp) are unaffected.  The context is process-wide (the
+    autograd engine runs GPU backwards on its own threads).  An extension of the
+    reference API."""
 
     def __init__(self, sink):
         self.sink = sink
 
     def __enter__(self):
-        stack = getattr(_tls, "sinks", None)
-        if stack is None:
-            stack = _tls.sinks = []
-        stack.append(self.sink)
+        with _SINKS_LOCK:
+            _SINKS.append(self.sink)
         return self.sink
 
     def __exit__(self, *exc):
-        _tls.sinks.pop()
+        with _SINKS_LOCK:
+            _SINKS.remove(self.sink)
         return False
 
 
 def _sh_sink():
-    stack = getattr(_tls, "sinks", None)
-    return stack[-1] if stack else None
+    with _SINKS_LOCK:
+        return _SINKS[-1] if _SINKS else None
 
 
 def _backward_views(views, means3D, colors_precomp, segments, scales, rotations, scale_modifier, cov3Ds_precomp,

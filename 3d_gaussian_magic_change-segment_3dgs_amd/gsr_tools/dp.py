@@ -131,6 +131,9 @@ class ShExchange:
                                  dmeans3D=dmeans3D, arena=arena))
 
     def start(self):
+        if not self.entries:
+            raise RuntimeError("ShExchange.start(): no deferred backward was recorded (run the backward inside "
+                               "diff_gaussian_rasterization.defer_sh_gradients(exchange))")
         entries, self.entries = self.entries, []
         return _ShExchangeHandle([self._start_one(e) for e in entries])
 
