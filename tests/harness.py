@@ -82,11 +82,11 @@ def _num_rendered(fn):
 
 
 def untile_n_contrib(tiles, W, H):
-    """[T,256] tile-major n_contrib (entry k*64 + lane, pixel row 16ty + 4k + (lane>>4),
-    col 16tx + (lane&15)) -> [H, W] image layout."""
+    """[T,256] tile-major n_contrib in the forward's quadrant layout (entry 64k + lane:
+    pixel row 16ty + 8(k>>1) + (lane>>3), col 16tx + 8(k&1) + (lane&7)) -> [H, W]."""
     gx, gy = (W + 15) // 16, (H + 15) // 16
-    t = tiles.reshape(gy, gx, 4, 4, 16)          # [ty, tx, k, r, c]
-    img = t.transpose(0, 2, 3, 1, 4).reshape(gy * 16, gx * 16)  # row-in-tile = 4k + r
+    t = tiles.reshape(gy, gx, 2, 2, 8, 8)        # [ty, tx, kr, kc, r, c]
+    img = t.transpose(0, 2, 4, 1, 3, 5).reshape(gy * 16, gx * 16)
     return img[:H, :W]
 
 
