@@ -268,19 +268,18 @@ static std::string g_err;
 static int g_exp_libm = 0;
 static inline float gsr_expf(float x) {
     // exp(clamp(x, -87, 88)): k = round(x log2 e) by the 1.5*2^23 shifter, Cody-Waite
-    // reduction, degree-7 Taylor polynomial (Horner, FMA), times 2^k built from the
+    // reduction, degree-6 minimax polynomial (Horner, FMA), times 2^k built from the
     // shifter's low bits.  Must stay bit-identical to render.hip: gsr_expf.
     const float xc = std::fmin(std::fmax(x, -87.0f), 88.0f);
     const float kf = std::fma(xc, 1.44269502f, 12582912.0f);
     const float k = kf - 12582912.0f;
     float r = std::fma(-k, 0.693145751953125f, xc);
     r = std::fma(-k, 1.42860677e-06f, r);
-    float p = 1.98412701e-04f;
-    p = std::fma(p, r, 1.38888892e-03f);
-    p = std::fma(p, r, 8.33333377e-03f);
-    p = std::fma(p, r, 4.16666679e-02f);
-    p = std::fma(p, r, 1.66666672e-01f);
-    p = std::fma(p, r, 0.5f);
+    float p = 0.001381461275741458f;  // degree-6 minimax (1 + r + c2 r^2 + ... + c6 r^6)
+    p = std::fma(p, r, 0.008368710055947304f);
+    p = std::fma(p, r, 0.04166838899254799f);
+    p = std::fma(p, r, 0.1666652113199234f);
+    p = std::fma(p, r, 0.4999999403953552f);
     p = std::fma(p, r, 1.0f);
     p = std::fma(p, r, 1.0f);
     uint32_t kb;
