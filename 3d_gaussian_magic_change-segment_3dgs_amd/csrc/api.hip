@@ -236,7 +236,8 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
         StageScope sc(GSR_STAGE_DEPTH_SORT, st);
         launch_radix_sort(at<uint32_t>(g, L.depth_keys), nullptr, at<uint32_t>(g, L.dkeys_alt),
                           at<uint32_t>(g, L.order_alt), at<uint32_t>(g, L.depth_keys), at<uint32_t>(g, L.order), P,
-                          32, g + L.ws, /*ws_zeroed=*/true, st);
+                          32, g + L.ws, /*ws_zeroed=*/true, st, nullptr, nullptr, nullptr, nullptr,
+                          /*skip_sentinel=*/true);  // culled Gaussians (key ~0u) emit nothing
     }
     GSR_STAGE("depth sort");
     {
@@ -295,23 +296,25 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
             // key = tile, payload = (instance slot u, Gaussian id): the slot orders ties by
             // (depth, gaussian); the id travels along so point_list needs no gather.
             StageScope sc(GSR_STAGE_TILE_SORT, st);
+            // the last pass also produces the tile ranges (identifyTileRanges,
+            // rasterizer_impl.cu:113-138) and clears the backward's written-slot mask
+            const SortFinal fin{ranges, at<uint4>(b, BL.written), cdiv(I, 128)};
             launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout, at<uint32_t>(b, BL.slot_vals),
                               I, bits, b + BL.ws, /*ws_zeroed=*/false, st,
                               at<uint32_t>(b, BL.slot_gid), at<uint32_t>(b, BL.gid_alt),
-                              at<uint32_t>(b, BL.point_list));
+                              at<uint32_t>(b, BL.point_list), &fin);
         }
         GSR_STAGE("tile sort");
         point_list = at<uint32_t>(b, BL.point_list);
-        {
-            StageScope sc(GSR_STAGE_RANGES, st);
-            launch_finalize(I, kout, ranges, at<uint32_t>(b, BL.written), st);
-        }
-        GSR_STAGE("tile ranges");
     }
     uint32_t* order = at<uint32_t>(im, IL.order);
     {
-        StageScope sc(GSR_STAGE_RENDER_FWD, st);
+        StageScope sc(GSR_STAGE_RANGES, st);
         launch_tile_order(ranges, T, order, st);
+    }
+    GSR_STAGE("tile order");
+    {
+        StageScope sc(GSR_STAGE_RENDER_FWD, st);
         launch_render_forward(s->W, s->H, IL.gx, IL.gy, order, ranges, point_list,
                               g ? at<float4>(g, GL.rec) : nullptr, s->bg, out_color, out_depth, out_alpha,
                               out_segment, at<uint32_t>(im, IL.n_contrib), st);
@@ -346,7 +349,7 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
         const BinLayout BL = bin_layout(I);
         char* b = aligned_base(binning);
         contrib = reinterpret_cast<float*>(aligned_base(scratch));
-        written = at<uint32_t>(b, BL.written);  // cleared by the forward's k_finalize
+        written = at<uint32_t>(b, BL.written);  // cleared by the forward's tile sort
         {
             StageScope sc(GSR_STAGE_RENDER_BWD, st);
             launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order), at<uint2>(im, IL.ranges),

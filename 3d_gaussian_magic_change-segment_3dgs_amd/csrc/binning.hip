@@ -192,25 +192,65 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restric
 // ---------------------------------------------------------- radix sort ----
 // Digit histograms of every pass at once (one read of the keys): LDS counters per
 // block, then one global atomic per (pass, digit, block).  hist[p * RADIX + d].
+// Also the digit range of every pass over the keys that matter (all keys, or all but
+// the 0xFFFFFFFF sentinel when skip_sentinel: culled Gaussians of the depth sort, whose
+// position is irrelevant): span[2p] = max(256 - d), span[2p + 1] = max(d + 1) (zero-
+// initialised words).  A pass whose keys that matter all share one digit is the
+// identity on them and is skipped (k_radix_scatter copies the tile through).
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __restrict__ keys, size_t n,
                                                              int passes, int per_pass, int key_bits,
-                                                             uint32_t* __restrict__ hist) {
+                                                             uint32_t* __restrict__ hist, uint32_t* span,
+                                                             int skip_sentinel) {
     __shared__ uint32_t cnt[4][RADIX];
+    __shared__ uint32_t s_span[8];
 #pragma unroll
     for (int p = 0; p < 4; ++p) cnt[p][threadIdx.x] = 0;
+    if (threadIdx.x < 8) s_span[threadIdx.x] = 0;
     __syncthreads();
-    for (size_t idx = (size_t)blockIdx.x * SORT_THREADS + threadIdx.x; idx < n;
+    uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};  // max(256 - d), max(d + 1)
+    // Wave-aggregated counting: a digit shared by the whole wave (the high digits of keys
+    // with a narrow range) is one LDS atomic, not 64 serialised ones on one address.
+    const size_t n_round = (n + 63) & ~(size_t)63;
+    for (size_t idx = (size_t)blockIdx.x * SORT_THREADS + threadIdx.x; idx < n_round;
          idx += (size_t)gridDim.x * SORT_THREADS) {
-        const uint32_t k = keys[idx];
-        for (int p = 0; p < passes; ++p) {
+        const bool valid = idx < n;
+        const uint32_t k = valid ? keys[idx] : 0u;
+        const uint64_t vmask = __ballot(valid);
+        const bool matters = valid && !(skip_sentinel && k == 0xFFFFFFFFu);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+            if (p >= passes) break;
             const int shift = p * per_pass;
             const int bits = min(per_pass, key_bits - shift);
-            atomicAdd(&cnt[p][(k >> shift) & ((1u << bits) - 1u)], 1u);
+            const uint32_t d = (k >> shift) & ((1u << bits) - 1u);
+            if (matters) {
+                lo[p] = max(lo[p], 256u - d);
+                hi[p] = max(hi[p], d + 1u);
+            }
+            const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
+            if (__ballot(valid && d == d0) == vmask) {
+                if ((threadIdx.x & 63) == 0) atomicAdd(&cnt[p][d0], (uint32_t)__popcll(vmask));
+            } else if (valid) {
+                atomicAdd(&cnt[p][d], 1u);
+            }
+        }
+    }
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) {
+            lo[p] = max(lo[p], (uint32_t)__shfl_xor((int)lo[p], o, 64));
+            hi[p] = max(hi[p], (uint32_t)__shfl_xor((int)hi[p], o, 64));
+        }
+        if ((threadIdx.x & 63) == 0 && p < passes) {
+            atomicMax(&s_span[2 * p], lo[p]);
+            atomicMax(&s_span[2 * p + 1], hi[p]);
         }
     }
     __syncthreads();
     for (int p = 0; p < passes; ++p)
         if (cnt[p][threadIdx.x]) atomicAdd(&hist[p * RADIX + threadIdx.x], cnt[p][threadIdx.x]);
+    if (threadIdx.x < 2 * passes && s_span[threadIdx.x]) atomicMax(&span[threadIdx.x], s_span[threadIdx.x]);
 }
 
 // Per-tile digit histogram -> hist[digit * ntiles + tile] (table-driven passes).
@@ -271,15 +311,37 @@ template <int ITEMS, int WAVES, bool LB>
 __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, size_t n, int shift, int bits, const uint32_t* __restrict__ hist,
-    uint64_t* status, uint32_t* counter, const uint32_t* __restrict__ vals2_in, uint32_t* __restrict__ vals2_out) {
+    uint64_t* status, uint32_t* counter, const uint32_t* __restrict__ vals2_in, uint32_t* __restrict__ vals2_out,
+    SortFinal fin, const uint32_t* span) {
     constexpr int NT = 64 * WAVES, TILE = NT * ITEMS;
+    for (size_t i = (size_t)blockIdx.x * NT + threadIdx.x; i < fin.zero16; i += (size_t)gridDim.x * NT)
+        fin.zero[i] = make_uint4(0u, 0u, 0u, 0u);
     __shared__ uint32_t s_key[TILE], s_val[TILE], s_val2[TILE];
     __shared__ uint32_t wcnt[WAVES][RADIX];
     __shared__ uint32_t dbase[RADIX], gbase[RADIX];
     __shared__ uint32_t wsum[WAVES];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t ndig = 1u << bits, mask = ndig - 1u;
+    // span = this pass's digit range over the keys that matter (k_radix_hist)
+    const uint32_t sp_lo = LB && span ? span[0] : 0u, sp_hi = LB && span ? span[1] : 1u;
     const int t = LB ? lb_tile_index(counter) : (int)blockIdx.x;
+    if (LB && span && (sp_lo == 0u || 256u - sp_lo == sp_hi - 1u)) {
+        // Every key that matters has the same digit in this pass: a stable pass is the
+        // identity on them, so the tile is copied through and the look-back chain is
+        // skipped.  Uniform over the grid.
+        for (size_t idx = (size_t)blockIdx.x * TILE + tid; idx < min(n, (size_t)(blockIdx.x + 1) * TILE);
+             idx += NT) {
+            const uint32_t k = keys_in[idx];
+            if (keys_out) keys_out[idx] = k;
+            vals_out[idx] = vals_in ? vals_in[idx] : (uint32_t)idx;
+            if (vals2_out) vals2_out[idx] = vals2_in[idx];
+            if (fin.ranges) {
+                if (idx == 0 || keys_in[idx - 1] != k) atomicMin(&fin.ranges[k].x, (uint32_t)idx);
+                if (idx == n - 1 || keys_in[idx + 1] != k) atomicMax(&fin.ranges[k].y, (uint32_t)(idx + 1));
+            }
+        }
+        return;
+    }
 #pragma unroll
     for (int i = 0; i < RADIX / 64; ++i) wcnt[wid][lane + 64 * i] = 0;
     const size_t bbase = (size_t)t * TILE;
@@ -363,9 +425,15 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
         const uint32_t k = s_key[p];
         const uint32_t d = (k >> shift) & mask;
         const size_t g = (size_t)gbase[d] + (uint32_t)p - dbase[d];
-        keys_out[g] = k;
+        if (keys_out) keys_out[g] = k;
         vals_out[g] = s_val[p];
         if (vals2_out) vals2_out[g] = s_val2[p];
+        if (fin.ranges) {
+            // Last pass: the tile is in final order, so equal keys are adjacent here and a
+            // key's run continues across tiles only at the tile's ends.
+            if (p == 0 || s_key[p - 1] != k) atomicMin(&fin.ranges[k].x, (uint32_t)g);
+            if (p == nvalid - 1 || s_key[p + 1] != k) atomicMax(&fin.ranges[k].y, (uint32_t)(g + 1));
+        }
     }
 }
 
@@ -384,9 +452,10 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
                                                    uint32_t* __restrict__ tkeys, uint32_t* __restrict__ slot_gid,
                                                    uint32_t* __restrict__ goff, uint2* __restrict__ ranges, int T) {
     __shared__ uint32_t s_key[DUP_CAP], s_gid[DUP_CAP];
-    // empty tiles keep ranges {0, 0} (rasterizer_impl.cu:316 memset), set here
+    // ranges start at {~0u, 0} for the tile sort's atomicMin / atomicMax; empty tiles end
+    // up {0, 0} (rasterizer_impl.cu:316 memset) in k_tile_order
     for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < T; i += gridDim.x * blockDim.x)
-        ranges[i] = make_uint2(0u, 0u);
+        ranges[i] = make_uint2(~0u, 0u);
     const int r0 = blockIdx.x * blockDim.x;
     const int r = r0 + threadIdx.x;
     const int rl = min(r0 + (int)blockDim.x, P) - 1;
@@ -425,33 +494,24 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
     }
 }
 
-// Tile ranges [first, last+1) from the sorted tile keys (identifyTileRanges,
-// rasterizer_impl.cu:113-138).
-__global__ void __launch_bounds__(256) k_finalize(size_t I, const uint32_t* __restrict__ tkeys,
-                                                  uint2* __restrict__ ranges, uint32_t* __restrict__ written) {
-    const size_t k = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
-    // the backward's written-slot mask starts empty
-    if (k < cdiv(I, 128)) reinterpret_cast<uint4*>(written)[k] = make_uint4(0u, 0u, 0u, 0u);
-    if (k >= I) return;
-    const uint32_t t = tkeys[k];
-    if (k == 0 || tkeys[k - 1] != t) ranges[t].x = (uint32_t)k;
-    if (k == I - 1 || tkeys[k + 1] != t) ranges[t].y = (uint32_t)(k + 1);
-}
-
 // Heavy-first tile schedule for the render kernels: tiles bucketed by the bit
 // length of their instance count, longest bucket first.  The hardware dispatcher
 // hands workgroups out in index order as slots free up, so issuing the heavy
 // tiles first turns it into a longest-processing-time-first scheduler (the
 // natural row-major order leaves the dense centre tiles for the end).  Order
 // within a bucket is arbitrary: it changes timing only, never a result.
-__global__ void __launch_bounds__(1024) k_tile_order(const uint2* __restrict__ ranges, int T,
+__global__ void __launch_bounds__(1024) k_tile_order(uint2* __restrict__ ranges, int T,
                                                      uint32_t* __restrict__ order) {
     __shared__ uint32_t hist[33], off[33];
     const int tid = threadIdx.x;
     if (tid < 33) hist[tid] = 0;
     __syncthreads();
     for (int t = tid; t < T; t += blockDim.x) {
-        const uint2 r = ranges[t];
+        uint2 r = ranges[t];
+        if (r.x == ~0u) {  // no instance (the tile sort's atomicMin never touched it): {0, 0}
+            r = make_uint2(0u, 0u);
+            ranges[t] = r;
+        }
         const uint32_t len = r.y - r.x;
         atomicAdd(&hist[len ? 32 - __clz(len) : 0], 1u);
     }
@@ -523,11 +583,12 @@ bool sort_uses_lookback(size_t n) { return n <= g_sort_lb_max; }
 template <int ITEMS, int WAVES, bool LB>
 static void launch_scatter(size_t n, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
                            int shift, int bits, const uint32_t* hist, uint64_t* status, uint32_t* counter,
-                           const uint32_t* v2in, uint32_t* v2out, hipStream_t st) {
+                           const uint32_t* v2in, uint32_t* v2out, SortFinal fin, const uint32_t* span,
+                           hipStream_t st) {
     static_assert(WAVES * ITEMS % 4 == 0, "tile must be a multiple of 256 elements");
     hipLaunchKernelGGL((k_radix_scatter<ITEMS, WAVES, LB>), dim3(sort_tiles(n, WAVES * ITEMS / 4)),
                        dim3(64 * WAVES), 0, st, kin, vin, kout, vout, n, shift, bits, hist, status, counter, v2in,
-                       v2out);
+                       v2out, fin, span);
 }
 
 // Stable LSD sort of (keys, vals[, vals2]) on the low key_bits bits.  Ping-pongs
@@ -535,7 +596,8 @@ static void launch_scatter(size_t n, const uint32_t* kin, const uint32_t* vin, u
 // keys_in / vals_in / vals2_in are not modified.
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_tmp, uint32_t* vals_tmp,
                        uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits, void* ws, bool ws_zeroed,
-                       hipStream_t st, const uint32_t* vals2_in, uint32_t* vals2_tmp, uint32_t* vals2_out) {
+                       hipStream_t st, const uint32_t* vals2_in, uint32_t* vals2_tmp, uint32_t* vals2_out,
+                       const SortFinal* final_out, bool skip_sentinel) {
     if (n == 0) return;
     if (key_bits < 1) key_bits = 1;
     const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
@@ -546,7 +608,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);
         hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)min(nt, (size_t)1024)), dim3(SORT_THREADS), 0, st, keys_in,
-                           n, passes, per_pass, key_bits, W.hist);
+                           n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel);
     }
     const uint32_t* kin = keys_in;
     const uint32_t* vin = vals_in;
@@ -559,11 +621,15 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
         uint32_t* kout = to_out ? keys_out : keys_tmp;
         uint32_t* vout = to_out ? vals_out : vals_tmp;
         uint32_t* v2out = vals2_in ? (to_out ? vals2_out : vals2_tmp) : nullptr;
+        const bool last = p == passes - 1;
+        const SortFinal fin = (last && final_out) ? *final_out : SortFinal{nullptr, nullptr, 0};
+        if (fin.ranges) kout = nullptr;  // the ranges replace the sorted keys
         if (lb) {
             const size_t nt = sort_tiles(n, sort_lb_items());
             launch_scatter<GSR_LB_ITEMS, GSR_LB_WAVES, true>(n, kin, vin, kout, vout, shift, bits,
                                                              W.hist + p * RADIX, W.status + (size_t)p * nt * RADIX,
-                                                             W.counter + p, v2in, v2out, st);
+                                                             W.counter + p, v2in, v2out, fin,
+                                                             W.counter + SPAN_WORD + 2 * p, st);
         } else {
             const size_t nt = sort_tiles(n, GSR_TB_ITEMS * GSR_TB_WAVES / 4);
             const size_t len = ((size_t)1 << bits) * nt;
@@ -574,7 +640,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
             hipLaunchKernelGGL(k_scan<false>, dim3(cdiv(len, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, W.table,
                                nullptr, len, W.table, S.status, S.counter, nullptr);
             launch_scatter<GSR_TB_ITEMS, GSR_TB_WAVES, false>(n, kin, vin, kout, vout, shift, bits, W.table, nullptr,
-                                                              nullptr, v2in, v2out, st);
+                                                              nullptr, v2in, v2out, fin, nullptr, st);
         }
         kin = kout;
         vin = vout;
@@ -582,7 +648,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     }
 }
 
-void launch_tile_order(const uint2* ranges, int T, uint32_t* order, hipStream_t st) {
+void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st) {
     if (T == 0) return;
     hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ranges, T, order);
 }
@@ -595,9 +661,5 @@ void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, con
                        gx, tkeys, slot_gid, goff, ranges, T);
 }
 
-void launch_finalize(size_t I, const uint32_t* tkeys, uint2* ranges, uint32_t* written, hipStream_t st) {
-    if (I == 0) return;
-    hipLaunchKernelGGL(k_finalize, dim3(cdiv(I, 256)), dim3(256), 0, st, I, tkeys, ranges, written);
-}
 
 }  // namespace gsr

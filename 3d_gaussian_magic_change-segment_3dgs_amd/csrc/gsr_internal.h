@@ -56,6 +56,9 @@ inline ScanWs scan_ws(size_t n, void* p) {
     char* c = static_cast<char*>(p);
     return {p, scan_ws_bytes(n), reinterpret_cast<uint32_t*>(c), reinterpret_cast<uint64_t*>(c + ALIGN)};
 }
+// Sort workspace header: words [0, passes) are the look-back tile counters, words
+// [SPAN_WORD, SPAN_WORD + 2 passes) the per-pass digit spans (k_radix_hist).
+constexpr int SPAN_WORD = 16;
 struct SortWs {
     void* base;
     size_t header;      // bytes of counter + pass histograms
@@ -126,7 +129,7 @@ inline BinLayout bin_layout(size_t I) {
     L.slot_gid = take(I * 4);
     L.gid_alt = take(I * 4);
     L.point_list = take(I * 4);
-    L.written = take(cdiv(I, 128) * 16);  // backward: 1 bit per instance slot (zeroed by k_finalize)
+    L.written = take(cdiv(I, 128) * 16);  // backward: 1 bit per instance slot (zeroed by the tile sort's last pass)
     L.ws = take(sort_ws_bytes(I, MAX_SORT_PASSES));
     L.bytes = o + ALIGN;
     return L;
@@ -200,21 +203,30 @@ void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const
                               const float* contrib, const uint32_t* written, const float4* rec,
                               const gsr_grads& g, hipStream_t st);
 // binning.hip
+// Optional last-pass outputs of a sort: ranges[key] = [first, last + 1) of each key's run in
+// the sorted order (atomicMin/atomicMax per run and tile; empty keys keep {~0u, 0}, which
+// k_tile_order turns into {0, 0}); the sorted keys themselves are then not written.  zero
+// / zero16: a buffer of zero16 x 16 B cleared on the way.
+struct SortFinal {
+    uint2* ranges;
+    uint4* zero;
+    size_t zero16;
+};
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL = identity*/, uint32_t* keys_tmp,
                        uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,
                        void* ws, bool ws_zeroed, hipStream_t st, const uint32_t* vals2_in = nullptr,
-                       uint32_t* vals2_tmp = nullptr, uint32_t* vals2_out = nullptr);
+                       uint32_t* vals2_tmp = nullptr, uint32_t* vals2_out = nullptr, const SortFinal* fin = nullptr,
+                       bool skip_sentinel = false);
 int depth_sort_passes();
 int sort_lb_items();
 bool sort_uses_lookback(size_t n);
 void set_sort_lookback_max(size_t n);
-void launch_tile_order(const uint2* ranges, int T, uint32_t* order, hipStream_t st);
+void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st);
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
                                   void* ws, bool ws_zeroed, hipStream_t st, uint32_t* host_total = nullptr);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, int gx, uint32_t* tkeys, uint32_t* slot_gid, uint32_t* goff,
                       uint2* ranges, int T, hipStream_t st);
-void launch_finalize(size_t I, const uint32_t* tkeys, uint2* ranges, uint32_t* written, hipStream_t st);
 // render.hip
 void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
                            const uint32_t* point_list,

@@ -57,7 +57,7 @@ EXCHANGE_DESC = {
 }
 
 
-def algorithmic_bytes(stage, P, I, HW, deg, views=1):
+def algorithmic_bytes(stage, P, I, HW, deg, views=1, T=0):
     """Bytes a stage must move per launch: SURVEY.md s8(d)'s per-unit figures
     (a7..a16) attributed to the gsr stage that does that work."""
     M = (deg + 1) ** 2
@@ -69,10 +69,10 @@ def algorithmic_bytes(stage, P, I, HW, deg, views=1):
         return 16 * P
     if stage == "duplicate":       # a9: 20 B per Gaussian + 12 B per instance
         return 20 * P + 12 * I
-    if stage == "tile_sort":       # a10: one read + write of key + value per instance
-        return 24 * I
-    if stage == "ranges":          # a11
-        return 8 * I
+    if stage == "tile_sort":       # a10 + a11: one read + write of key + value per instance;
+        return 24 * I + 8 * I      # its last pass also emits the tile ranges (identifyTileRanges)
+    if stage == "ranges":          # heavy-first tile schedule (k_tile_order): ranges read + written, order
+        return 20 * T
     if stage == "render_fwd":      # a12: 52 B per instance + 32 B per pixel
         return 52 * I + 32 * HW
     if stage == "render_bwd":      # a14 (per-instance + per-pixel part)
@@ -294,7 +294,8 @@ def main():
             avg = sms[i] / scnt[i]
             stages[names[i]] = {"avg_ms": round(avg, 4), "ms_per_step": round(sms[i] / n_stage_steps, 4),
                                 "launches_per_step": scnt[i] / n_stage_steps,
-                                "gbs": round(algorithmic_bytes(names[i], P, I, HW, deg, B) / (avg * 1e-3) / 1e9, 1)}
+                                "gbs": round(algorithmic_bytes(names[i], P, I, HW, deg, B, T=((W + 15) // 16) * ((H + 15) // 16))
+                                             / (avg * 1e-3) / 1e9, 1)}
     dom = names[dom_i] if stages else None
     value = world * B * args.steps / elapsed
     roof = None
