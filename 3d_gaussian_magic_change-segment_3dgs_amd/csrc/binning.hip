@@ -81,6 +81,64 @@ __device__ __forceinline__ uint32_t lb_lookback(uint64_t* col, size_t stride, in
     }
     return excl;
 }
+// The same, reading 8 predecessors per dependent step (one thread per column; used by
+// the radix scatter, where 256 digit columns walk back in parallel).
+__device__ __forceinline__ uint32_t lb_lookback8(uint64_t* col, size_t stride, int t) {
+    uint32_t excl = 0;
+    int i = t - 1;
+    while (true) {
+        uint64_t w[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int j = i - k;
+            w[k] = j >= 0 ? lb_load(col + (size_t)j * stride) : LB_PRE;
+        }
+        int consumed = 0;
+        bool done = false, stall = false;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            if (done || stall) continue;
+            const uint32_t f = (uint32_t)(w[k] >> 32);
+            if (f == 0) {
+                stall = true;
+                continue;
+            }
+            excl += (uint32_t)w[k];
+            ++consumed;
+            done = f == 2;
+        }
+        if (done) return excl;
+        i -= consumed;
+        if (stall) __builtin_amdgcn_s_sleep(1);
+    }
+}
+// The same, by a whole wave over a window of 64 predecessors per step: lane l inspects
+// tile i - l; the window is summed up to the nearest inclusive prefix (tiles below 0
+// count as an inclusive 0).  A window with an unpublished tile before that point is
+// re-read.  O(t / 64) dependent loads instead of O(t) when many tiles start together.
+__device__ __forceinline__ uint32_t lb_lookback_wave(uint64_t* col, int t) {
+    const int lane = threadIdx.x & 63;
+    uint32_t excl = 0;
+    int i = t - 1;
+    while (true) {
+        const int j = i - lane;
+        const uint64_t w = j >= 0 ? lb_load(col + j) : LB_PRE;
+        const uint32_t f = (uint32_t)(w >> 32);
+        const uint64_t inc = __ballot(f == 2u), unpub = __ballot(f == 0u);
+        const int stop = inc ? (int)__builtin_ctzll(inc) : 63;
+        const uint64_t need = stop == 63 ? ~0ull : ((2ull << stop) - 1ull);
+        if (unpub & need) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        uint32_t v = lane <= stop ? (uint32_t)w : 0u;
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) v += (uint32_t)__shfl_xor((int)v, o, 64);
+        excl += v;
+        if (inc) return excl;
+        i -= 64;
+    }
+}
 __device__ __forceinline__ int lb_tile_index(uint32_t* counter) {
     __shared__ int s_tile;
     if (threadIdx.x == 0) s_tile = (int)atomicAdd(counter, 1u);
@@ -157,16 +215,16 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restric
     }
     uint32_t total;
     uint32_t pre = block_exclusive_scan(sum, wsum, &total);
-    if (threadIdx.x == 0) {
+    if (threadIdx.x < 64) {  // wave 0: publish, look back over 64 tiles at a time, publish
         uint32_t excl = 0;
         if (t == 0) {
-            lb_store(status, LB_PRE | total);
+            if (threadIdx.x == 0) lb_store(status, LB_PRE | total);
         } else {
-            lb_store(status + t, LB_AGG | total);
-            excl = lb_lookback(status, 1, t);
-            lb_store(status + t, LB_PRE | (excl + total));
+            if (threadIdx.x == 0) lb_store(status + t, LB_AGG | total);
+            excl = lb_lookback_wave(status, t);
+            if (threadIdx.x == 0) lb_store(status + t, LB_PRE | (excl + total));
         }
-        s_excl = excl;
+        if (threadIdx.x == 0) s_excl = excl;
     }
     __syncthreads();
     pre += s_excl;
@@ -208,13 +266,21 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __r
     if (threadIdx.x < 8) s_span[threadIdx.x] = 0;
     __syncthreads();
     uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};  // max(256 - d), max(d + 1)
-    // Wave-aggregated counting: a digit shared by the whole wave (the high digits of keys
-    // with a narrow range) is one LDS atomic, not 64 serialised ones on one address.
-    const size_t n_round = (n + 63) & ~(size_t)63;
-    for (size_t idx = (size_t)blockIdx.x * SORT_THREADS + threadIdx.x; idx < n_round;
-         idx += (size_t)gridDim.x * SORT_THREADS) {
+    // HIST_ITEMS keys per thread, all loads issued before any use (a strided loop with
+    // one dependent load per iteration is latency-bound).
+    constexpr int HIST_ITEMS = 16;
+    const size_t base = (size_t)blockIdx.x * SORT_THREADS * HIST_ITEMS + threadIdx.x;
+    uint32_t kk[HIST_ITEMS];
+#pragma unroll
+    for (int i = 0; i < HIST_ITEMS; ++i) {
+        const size_t idx = base + (size_t)i * SORT_THREADS;
+        kk[i] = idx < n ? keys[idx] : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < HIST_ITEMS; ++i) {
+        const size_t idx = base + (size_t)i * SORT_THREADS;
         const bool valid = idx < n;
-        const uint32_t k = valid ? keys[idx] : 0u;
+        const uint32_t k = kk[i];
         const uint64_t vmask = __ballot(valid);
         const bool matters = valid && !(skip_sentinel && k == 0xFFFFFFFFu);
 #pragma unroll
@@ -227,9 +293,11 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __r
                 lo[p] = max(lo[p], 256u - d);
                 hi[p] = max(hi[p], d + 1u);
             }
+            // wave-aggregated: a digit shared by the whole wave (the high digits of keys
+            // with a narrow range) is one LDS atomic, not 64 serialised on one address
             const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
             if (__ballot(valid && d == d0) == vmask) {
-                if ((threadIdx.x & 63) == 0) atomicAdd(&cnt[p][d0], (uint32_t)__popcll(vmask));
+                if ((threadIdx.x & 63) == 0 && vmask) atomicAdd(&cnt[p][d0], (uint32_t)__popcll(vmask));
             } else if (valid) {
                 atomicAdd(&cnt[p][d], 1u);
             }
@@ -400,7 +468,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
                 lb_store(col, LB_PRE | tot);
             } else {
                 lb_store(col + (size_t)t * RADIX, LB_AGG | tot);
-                excl = lb_lookback(col, RADIX, t);
+                excl = lb_lookback8(col, RADIX, t);
                 lb_store(col + (size_t)t * RADIX, LB_PRE | (excl + tot));
             }
             gbase[tid] = gstart + excl;
@@ -607,7 +675,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     if (lb) {
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);
-        hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)min(nt, (size_t)1024)), dim3(SORT_THREADS), 0, st, keys_in,
+        hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)cdiv(n, (size_t)SORT_THREADS * 16)), dim3(SORT_THREADS), 0, st, keys_in,
                            n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel);
     }
     const uint32_t* kin = keys_in;

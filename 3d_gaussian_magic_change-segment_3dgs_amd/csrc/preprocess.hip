@@ -221,6 +221,22 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
         clamped[idx] = 0;
     }
 
+    // SH3 rows through LDS (below): the first half-run's loads are issued before the
+    // projection math so their latency overlaps it.
+    const bool sh_lds = in.colors_precomp == nullptr && s.M == 16 && (reinterpret_cast<uintptr_t>(in.shs) & 15) == 0;
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int wbase = blockIdx.x * blockDim.x + wave * 64;
+    float4 shv[6];
+    if (sh_lds) {
+        const float4* src = reinterpret_cast<const float4*>(in.shs + (size_t)wbase * 48);
+#pragma unroll
+        for (int r = 0; r < 6; ++r) {
+            const int f = lane + 64 * r;
+            const int row = f / 12;
+            shv[r] = (wbase + row < s.P) ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    }
+
     const f3 p_orig = ld3(in.means3D + 3 * (size_t)sidx);
     // in_frustum (auxiliary.h:139-164)
     const f3 p_view = xform4x3(p_orig, cam.view);
@@ -263,23 +279,28 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     if (in.colors_precomp == nullptr) {
         f3 dir = p_orig - cam.campos;
         dir = dir / sqrtf(dot3(dir, dir));
-        if (s.M == 16 && (reinterpret_cast<uintptr_t>(in.shs) & 15) == 0) {
+        if (sh_lds) {
             // SH3 rows (192 B) through LDS: the wave loads 32 rows at a time as
             // consecutive float4s (a thread loading its own row issues loads 192 B
             // apart: 0.056 ms of a 0.100 ms kernel at 1M), then the 32 owners evaluate
             // their colour from LDS.  Rows padded to 52 floats (2-way bank aliasing).
             __shared__ float shrow[4][32][52];
-            const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-            const int wbase = blockIdx.x * blockDim.x + wave * 64;
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int g0 = wbase + 32 * h;
-                const float4* src = reinterpret_cast<const float4*>(in.shs + (size_t)g0 * 48);
+                if (h == 1) {
+                    const float4* src = reinterpret_cast<const float4*>(in.shs + (size_t)g0 * 48);
+#pragma unroll
+                    for (int r = 0; r < 6; ++r) {
+                        const int f = lane + 64 * r;
+                        shv[r] = (g0 + f / 12 < s.P) ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+                    }
+                }
 #pragma unroll
                 for (int r = 0; r < 6; ++r) {
                     const int f = lane + 64 * r;  // float4 index in the 32-row run
                     const int row = f / 12, col = f - 12 * (f / 12);
-                    if (g0 + row < s.P) *reinterpret_cast<float4*>(&shrow[wave][row][4 * col]) = src[f];
+                    *reinterpret_cast<float4*>(&shrow[wave][row][4 * col]) = shv[r];
                 }
                 __syncthreads();
                 if ((lane >> 5) == h && ok) {
@@ -309,8 +330,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     float4* R = rec + (size_t)idx * REC_F4;
     R[0] = make_float4(px, py, conic_x, conic_y);
     R[1] = make_float4(conic_z, opacity, p_view.z, s0);
-    R[2] = make_float4(rgb.x, rgb.y, rgb.z, s1);
-    R[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    R[2] = make_float4(rgb.x, rgb.y, rgb.z, s1);  // R[3]: padding to 64 B, never read
     radii[idx] = (int)my_radius;
     tiles_touched[idx] = ntiles;
     depth_keys[idx] = __float_as_uint(p_view.z);
