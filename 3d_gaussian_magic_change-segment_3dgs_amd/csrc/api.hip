@@ -219,6 +219,7 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
     const ImgLayout IL = img_layout(s->W, s->H);
     const GeomLayout L = geom_layout(P);
     char* g = aligned_base(geom);
+    const bool packed = rect_packable(IL.gx, IL.gy);
     const HostSlot hs = host_total_slot();  // NULL views if pinned host memory is unavailable
     uint32_t* hslot = hs.host;
     if (hslot) __atomic_store_n(hslot, TOTAL_PENDING, __ATOMIC_RELAXED);
@@ -227,6 +228,7 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
         const bool lb = sort_uses_lookback(P);
         launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
                           at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect),
+                          packed ? at<uint32_t>(g, L.rect32) : nullptr,
                           g + L.ws, lb ? sort_lb_zero_bytes(P, depth_sort_passes(), sort_lb_items()) : 0,
                           g + L.ws_scan, scan_ws_bytes(P), st);
     }
@@ -236,14 +238,21 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
         StageScope sc(GSR_STAGE_DEPTH_SORT, st);
         launch_radix_sort(at<uint32_t>(g, L.depth_keys), nullptr, at<uint32_t>(g, L.dkeys_alt),
                           at<uint32_t>(g, L.order_alt), at<uint32_t>(g, L.depth_keys), at<uint32_t>(g, L.order), P,
-                          32, g + L.ws, /*ws_zeroed=*/true, st, nullptr, nullptr, nullptr, nullptr,
+                          32, g + L.ws, /*ws_zeroed=*/true, st, packed ? at<uint32_t>(g, L.rect32) : nullptr,
+                          packed ? at<uint32_t>(g, L.rect32_alt) : nullptr,
+                          packed ? at<uint32_t>(g, L.rect32_sorted) : nullptr, nullptr,
                           /*skip_sentinel=*/true);  // culled Gaussians (key ~0u) emit nothing
     }
     GSR_STAGE("depth sort");
     {
         StageScope sc(GSR_STAGE_SCAN, st);
-        launch_scan_inclusive_gather(at<uint32_t>(g, L.tiles_touched), at<uint32_t>(g, L.order),
-                                     at<uint32_t>(g, L.offsets), P, g + L.ws_scan, /*ws_zeroed=*/true, st, hs.dev);
+        if (packed)  // tile counts from the depth-ordered packed rects: no gather
+            launch_scan_inclusive_gather(at<uint32_t>(g, L.rect32_sorted), nullptr, at<uint32_t>(g, L.offsets), P,
+                                         g + L.ws_scan, /*ws_zeroed=*/true, st, hs.dev, /*rect_mode=*/true);
+        else
+            launch_scan_inclusive_gather(at<uint32_t>(g, L.tiles_touched), at<uint32_t>(g, L.order),
+                                         at<uint32_t>(g, L.offsets), P, g + L.ws_scan, /*ws_zeroed=*/true, st,
+                                         hs.dev);
     }
     GSR_STAGE("scan");
     uint32_t total = 0;
@@ -280,7 +289,8 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
         {
             StageScope sc(GSR_STAGE_DUPLICATE, st);
             launch_duplicate(P, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets),
-                             at<uint32_t>(g, GL.tiles_touched), at<ushort4>(g, GL.rect), IL.gx,
+                             at<uint32_t>(g, GL.tiles_touched), at<ushort4>(g, GL.rect),
+                             rect_packable(IL.gx, IL.gy) ? at<uint32_t>(g, GL.rect32_sorted) : nullptr, IL.gx,
                              at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid), at<uint32_t>(g, GL.goff),
                              ranges, T, st);
         }

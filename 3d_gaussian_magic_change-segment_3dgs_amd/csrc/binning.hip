@@ -178,7 +178,7 @@ template <bool INCLUSIVE>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restrict__ src,
                                                        const uint32_t* __restrict__ gather, size_t n,
                                                        uint32_t* __restrict__ out, uint64_t* status,
-                                                       uint32_t* counter, uint32_t* host_total) {
+                                                       uint32_t* counter, uint32_t* host_total, int rect_mode) {
     __shared__ uint32_t tile[SCAN_TILE + SCAN_TILE / 32];
     __shared__ uint32_t wsum[4];
     __shared__ uint32_t s_excl;
@@ -204,6 +204,10 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restric
             const size_t idx = base + i * SCAN_THREADS + threadIdx.x;
             v[i] = idx < n ? src[idx] : 0u;
         }
+        if (rect_mode)  // packed rect -> tile count (x1 - x0)(y1 - y0)
+#pragma unroll
+            for (int i = 0; i < SCAN_ITEMS; ++i)
+                v[i] = (((v[i] >> 16) & 255u) - (v[i] & 255u)) * ((v[i] >> 24) - ((v[i] >> 8) & 255u));
     }
 #pragma unroll
     for (int i = 0; i < SCAN_ITEMS; ++i) tile[pad(i * SCAN_THREADS + threadIdx.x)] = v[i];
@@ -516,7 +520,8 @@ constexpr int DUP_CAP = 4096;
 __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __restrict__ order,
                                                    const uint32_t* __restrict__ offsets,
                                                    const uint32_t* __restrict__ tiles_touched,
-                                                   const ushort4* __restrict__ rect, int gx,
+                                                   const ushort4* __restrict__ rect,
+                                                   const uint32_t* __restrict__ rect_sorted, int gx,
                                                    uint32_t* __restrict__ tkeys, uint32_t* __restrict__ slot_gid,
                                                    uint32_t* __restrict__ goff, uint2* __restrict__ ranges, int T) {
     __shared__ uint32_t s_key[DUP_CAP], s_gid[DUP_CAP];
@@ -532,11 +537,20 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
     const bool staged = bend - bbase <= (uint32_t)DUP_CAP;
     if (r < P) {
         const uint32_t g = order[r];
-        const uint32_t cnt = tiles_touched[g];
+        // packed rect in depth order (coalesced) when available, else gathered by id
+        ushort4 rc;
+        uint32_t cnt;
+        if (rect_sorted) {
+            const uint32_t pr = rect_sorted[r];
+            rc = make_ushort4(pr & 255u, (pr >> 8) & 255u, (pr >> 16) & 255u, pr >> 24);
+            cnt = (uint32_t)(rc.z - rc.x) * (uint32_t)(rc.w - rc.y);
+        } else {
+            cnt = tiles_touched[g];
+            rc = cnt ? rect[g] : make_ushort4(0, 0, 0, 0);
+        }
         if (cnt != 0) {
             uint32_t off = r == 0 ? 0u : offsets[r - 1];
             goff[g] = off;
-            const ushort4 rc = rect[g];
             if (staged) {
                 uint32_t lo = off - bbase;
                 for (int y = rc.y; y < rc.w; ++y)
@@ -613,12 +627,12 @@ uint32_t higher_msb(uint32_t n) {
 }
 
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
-                                  void* ws, bool ws_zeroed, hipStream_t st, uint32_t* host_total) {
+                                  void* ws, bool ws_zeroed, hipStream_t st, uint32_t* host_total, bool rect_mode) {
     if (n == 0) return;
     const ScanWs W = scan_ws(n, ws);
     if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, W.bytes, st);
     hipLaunchKernelGGL(k_scan<true>, dim3(cdiv(n, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, src, gather_idx, n, out,
-                       W.status, W.counter, host_total);
+                       W.status, W.counter, host_total, (int)rect_mode);
 }
 
 // Sorting modes (measured on MI355X): small sorts are launch-bound and use one
@@ -706,7 +720,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
                                kin, n, shift,
                                bits, W.table, S.base, cdiv(S.bytes, 16));
             hipLaunchKernelGGL(k_scan<false>, dim3(cdiv(len, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, W.table,
-                               nullptr, len, W.table, S.status, S.counter, nullptr);
+                               nullptr, len, W.table, S.status, S.counter, nullptr, 0);
             launch_scatter<GSR_TB_ITEMS, GSR_TB_WAVES, false>(n, kin, vin, kout, vout, shift, bits, W.table, nullptr,
                                                               nullptr, v2in, v2out, fin, nullptr, st);
         }
@@ -722,11 +736,11 @@ void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st) {
 }
 
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
-                      const ushort4* rect, int gx, uint32_t* tkeys, uint32_t* slot_gid, uint32_t* goff,
-                      uint2* ranges, int T, hipStream_t st) {
+                      const ushort4* rect, const uint32_t* rect_sorted, int gx, uint32_t* tkeys,
+                      uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, hipStream_t st) {
     if (P == 0) return;
     hipLaunchKernelGGL(k_duplicate, dim3(cdiv(P, 256)), dim3(256), 0, st, P, order, offsets, tiles_touched, rect,
-                       gx, tkeys, slot_gid, goff, ranges, T);
+                       rect_sorted, gx, tkeys, slot_gid, goff, ranges, T);
 }
 
 

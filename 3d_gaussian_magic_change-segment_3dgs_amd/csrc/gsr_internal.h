@@ -92,7 +92,7 @@ inline SortWs sort_ws(size_t n, void* p) {
 // ---- geometry buffer (reference GeometryState, rasterizer_impl.cu:155-171) ----
 struct GeomLayout {
     size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, goff, ws,
-        ws_scan, bytes;
+        ws_scan, rect32, rect32_alt, rect32_sorted, bytes;
 };
 inline GeomLayout geom_layout(size_t P) {
     GeomLayout L{};
@@ -110,6 +110,12 @@ inline GeomLayout geom_layout(size_t P) {
     L.goff = take(P * 4);
     L.ws = take(sort_ws_bytes(P, MAX_SORT_PASSES));  // depth sort
     L.ws_scan = take(scan_ws_bytes(P));              // tiles_touched scan
+    // tile rect packed as x0 | y0 << 8 | x1 << 16 | y1 << 24 (grids up to 255 x 255 tiles):
+    // the depth sort carries it, so the scan and the duplicate read it in depth order
+    // instead of gathering tiles_touched[g] / rect[g] at random
+    L.rect32 = take(P * 4);
+    L.rect32_alt = take(P * 4);
+    L.rect32_sorted = take(P * 4);
     L.bytes = o + ALIGN;
     return L;
 }
@@ -166,8 +172,10 @@ inline char* aligned_base(void* p) {
 // preprocess.hip
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec,
                        int* radii, uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped,
-                       ushort4* rect, void* zero_a, size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes,
-                       hipStream_t st);
+                       ushort4* rect, uint32_t* rect32, void* zero_a, size_t zero_a_bytes, void* zero_b,
+                       size_t zero_b_bytes, hipStream_t st);
+// the packed rect (GeomLayout::rect32) fits grids of up to 255 x 255 tiles (4080 px)
+inline bool rect_packable(int gx, int gy) { return gx <= 255 && gy <= 255; }
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
 // Per-view inputs of the multi-view per-Gaussian backward (preprocess.hip).
 struct MvView {
@@ -222,11 +230,14 @@ int sort_lb_items();
 bool sort_uses_lookback(size_t n);
 void set_sort_lookback_max(size_t n);
 void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st);
+// value(j) = src[gather[j]] (gather != NULL), src[j], or, with rect_mode, the tile count
+// (x1 - x0)(y1 - y0) of the packed rect src[j]
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
-                                  void* ws, bool ws_zeroed, hipStream_t st, uint32_t* host_total = nullptr);
+                                  void* ws, bool ws_zeroed, hipStream_t st, uint32_t* host_total = nullptr,
+                                  bool rect_mode = false);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
-                      const ushort4* rect, int gx, uint32_t* tkeys, uint32_t* slot_gid, uint32_t* goff,
-                      uint2* ranges, int T, hipStream_t st);
+                      const ushort4* rect, const uint32_t* rect_sorted, int gx, uint32_t* tkeys,
+                      uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, hipStream_t st);
 // render.hip
 void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
                            const uint32_t* point_list,

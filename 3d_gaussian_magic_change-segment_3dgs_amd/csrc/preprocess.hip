@@ -203,6 +203,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
                                                     uint32_t* __restrict__ tiles_touched,
                                                     uint32_t* __restrict__ depth_keys,
                                                     uint8_t* __restrict__ clamped, ushort4* __restrict__ rect,
+                                                    uint32_t* __restrict__ rect32,
                                                     void* zero_a, size_t zero_a16, void* zero_b, size_t zero_b16) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     // clear the depth sort's and the scan's look-back counters (saves two memset launches)
@@ -219,6 +220,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
         tiles_touched[idx] = 0;
         depth_keys[idx] = 0xFFFFFFFFu;  // culled Gaussians sort last; they emit no instances
         clamped[idx] = 0;
+        if (rect32) rect32[idx] = 0u;   // empty rect: no tiles
     }
 
     // SH3 rows through LDS (below): the first half-run's loads are issued before the
@@ -336,6 +338,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     depth_keys[idx] = __float_as_uint(p_view.z);
     clamped[idx] = cbits;
     rect[idx] = make_ushort4((unsigned short)x0, (unsigned short)y0, (unsigned short)x1, (unsigned short)y1);
+    if (rect32) rect32[idx] = (uint32_t)x0 | ((uint32_t)y0 << 8) | ((uint32_t)x1 << 16) | ((uint32_t)y1 << 24);
 }
 
 // checkFrustum (rasterizer_impl.cu:54-66)
@@ -1045,11 +1048,12 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv_sh(int P, int D, i
 }  // namespace
 
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec, int* radii,
-                       uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped, ushort4* rect, void* zero_a,
-                       size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes, hipStream_t st) {
+                       uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped, ushort4* rect,
+                       uint32_t* rect32, void* zero_a, size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes,
+                       hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_preprocess, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, gx, gy, rec, radii,
-                       tiles_touched, depth_keys, clamped, rect, zero_a, cdiv(zero_a_bytes, 16), zero_b,
+                       tiles_touched, depth_keys, clamped, rect, rect32, zero_a, cdiv(zero_a_bytes, 16), zero_b,
                        cdiv(zero_b_bytes, 16));
 }
 
