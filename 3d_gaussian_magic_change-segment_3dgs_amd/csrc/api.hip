@@ -333,6 +333,16 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
     return 0;
 }
 
+int gsr_forward(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* binning,
+                size_t binning_bytes, void* img, float* out_color, float* out_depth, float* out_alpha,
+                float* out_segment, void* stream, int* num_rendered) {
+    if (int rc = gsr_forward_geometry(s, in, geom, radii, stream, num_rendered)) return rc;
+    if (*num_rendered > 0 && (binning == nullptr || gsr_binning_bytes(*num_rendered) > binning_bytes))
+        return GSR_NEED_BINNING;
+    return gsr_forward_render(s, in, geom, binning, img, *num_rendered, out_color, out_depth, out_alpha,
+                              out_segment, stream);
+}
+
 int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, void* geom, void* binning,
                  void* img, int num_rendered, const float* alpha, const float* dL_dcolor, const float* dL_dsegment,
                  const float* dL_ddepth, const float* dL_dalpha, void* scratch, const gsr_grads* grads,

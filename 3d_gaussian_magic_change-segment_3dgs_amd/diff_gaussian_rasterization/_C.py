@@ -61,6 +61,10 @@ _lib.gsr_forward_geometry.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(
 _lib.gsr_forward_render.restype = _i
 _lib.gsr_forward_render.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _vp, _vp, _vp, _i,
                                     _vp, _vp, _vp, _vp, _vp]
+_lib.gsr_forward.restype = _i
+_lib.gsr_forward.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _vp, _vp, _vp, _sz, _vp,
+                             _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_int)]
+GSR_NEED_BINNING = 2
 _lib.gsr_backward.restype = _i
 _lib.gsr_backward.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _vp, _vp, _vp, _vp, _i, _vp,
                               _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_Grads), _vp]
@@ -109,7 +113,7 @@ _lib.gsr_timing_collect.restype = _i
 _lib.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
 
 EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_img_bytes", "gsr_backward_scratch_bytes",
-                    "gsr_forward_geometry", "gsr_forward_render", "gsr_backward", "gsr_mark_visible",
+                    "gsr_forward_geometry", "gsr_forward_render", "gsr_forward", "gsr_backward", "gsr_mark_visible",
                     "gsr_debug_copy", "gsr_num_stages", "gsr_stage_name", "gsr_timing_enable", "gsr_timing_collect",
                     "gsr_last_error", "gsr_version", "gsr_set_option", "gsr_multiview_scratch_bytes",
                     "gsr_backward_multiview", "gsr_sh_rows_floats", "gsr_backward_multiview_deferred_sh",
@@ -255,15 +259,21 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
         cap = cap + cap // 7 + 4096 if cap and _BIN_GUESS else 0
         binning = torch.empty(_lib.gsr_binning_bytes(cap), **u8) if cap else None
         nr = ctypes.c_int(0)
-        _check(_lib.gsr_forward_geometry(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), radii.data_ptr(),
-                                         stream, ctypes.byref(nr)))
+        # geometry, the num_rendered sync and the render in one C call when the guess holds
+        rc = _lib.gsr_forward(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), radii.data_ptr(),
+                              binning.data_ptr() if binning is not None else None,
+                              binning.numel() if binning is not None else 0, img.data_ptr(), color.data_ptr(),
+                              depth.data_ptr(), alpha.data_ptr(), segment.data_ptr(), stream, ctypes.byref(nr))
         num_rendered = int(nr.value)
         _last_rendered[device] = num_rendered
-        if binning is None or num_rendered > cap:
+        if rc == GSR_NEED_BINNING:  # no guess, or too small: stage B with the exact size
             binning = torch.empty(_lib.gsr_binning_bytes(num_rendered), **u8)
-        _check(_lib.gsr_forward_render(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), binning.data_ptr(),
-                                       img.data_ptr(), num_rendered, color.data_ptr(), depth.data_ptr(),
-                                       alpha.data_ptr(), segment.data_ptr(), stream))
+            rc = _lib.gsr_forward_render(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), binning.data_ptr(),
+                                         img.data_ptr(), num_rendered, color.data_ptr(), depth.data_ptr(),
+                                         alpha.data_ptr(), segment.data_ptr(), stream)
+        _check(rc)
+        if binning is None:  # num_rendered == 0 with no guess
+            binning = torch.empty(0, **u8)
     return num_rendered, color, depth, segment, alpha, radii, geom, binning, img
 
 

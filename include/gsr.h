@@ -120,6 +120,18 @@ GSR_API int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void
                        void* img, int num_rendered, float* out_color, float* out_depth,
                        float* out_alpha, float* out_segment, void* stream);
 
+/* ---- forward, both stages in one call (Rasterizer::forward, rasterizer_impl.cu:
+ * 198-344): stage A, the num_rendered sync, then stage B straight from C when the
+ * caller's binning buffer (binning_bytes, e.g. a guess from the previous view) holds
+ * gsr_binning_bytes(num_rendered) -- no host-language round trip sits between the
+ * sync and the render launches.  Returns 0 (rendered), GSR_NEED_BINNING (stage A done,
+ * *num_rendered set, nothing rendered: call gsr_forward_render with a buffer of
+ * gsr_binning_bytes(*num_rendered)), or another nonzero error (gsr_last_error). */
+#define GSR_NEED_BINNING 2
+GSR_API int gsr_forward(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* binning,
+                        size_t binning_bytes, void* img, float* out_color, float* out_depth, float* out_alpha,
+                        float* out_segment, void* stream, int* num_rendered);
+
 /* ---- backward.  Replaces Rasterizer::backward (rasterizer_impl.cu:348-458) /
  * RasterizeGaussiansBackwardCUDA (rasterize_points.cu:127-221).  dL_d* are the
  * upstream image gradients (same shapes as the forward outputs); alpha is the
