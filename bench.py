@@ -29,6 +29,7 @@ Prints ONE JSON line on rank 0.  Extra objects:
                   same workload (whole views, rank 0, N = 1 only).
 """
 import argparse
+import gc
 import contextlib
 import json
 import math
@@ -238,7 +239,12 @@ def main():
     step = make_step(B)
 
     def timed(fn, k):
-        """k steps between a barrier + device sync on both sides; max over ranks."""
+        """k steps between a barrier + device sync on both sides; max over ranks.  Python's
+        cyclic GC is paused inside (collected just before): a collection pass in the
+        middle of the loop stalls the host for milliseconds, which leaves the GPU idle
+        behind the per-view num_rendered sync."""
+        gc.collect()
+        gc.disable()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
@@ -247,6 +253,7 @@ def main():
             fn()
         drain()
         torch.cuda.synchronize()
+        gc.enable()
         if dist is not None:
             dist.barrier()
         el = time.perf_counter() - t_start
