@@ -135,6 +135,33 @@ __device__ __forceinline__ M3 vrk_of(const float* c) {
 // a multiple of 4 floats (M = 16 in training) are fetched with 16-B loads: at a
 // 192-B stride between lanes every load instruction touches 64 cache lines, so 12
 // float4 loads cost a quarter of the memory-pipeline work of 48 dword loads.
+// Streaming hints: the forward's SH row loads and the backward's dsh row stores are
+// non-temporal (read / written once per view).  Measured at 1M, SH3: preprocess 83 -> 62 us,
+// per-Gaussian backward 152 -> 150 us.  The backward's own SH row loads stay ordinary:
+// non-temporal there cost 150 -> 220 us (thread-own 192-B rows re-touch each line 12 times).
+// GSR_NO_NT_SH restores ordinary accesses.
+#ifndef GSR_NO_NT_SH
+#define GSR_NT_SH_LOAD
+#define GSR_NT_SH_STORE
+#endif
+typedef float sh_v4 __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 sh_ld(const float4* p) {
+#ifdef GSR_NT_SH_LOAD
+    const sh_v4 r = __builtin_nontemporal_load(reinterpret_cast<const sh_v4*>(p));
+    return make_float4(r.x, r.y, r.z, r.w);
+#else
+    return *p;
+#endif
+}
+__device__ __forceinline__ void sh_st(float4* p, float4 v) {
+#ifdef GSR_NT_SH_STORE
+    const sh_v4 r = {v.x, v.y, v.z, v.w};
+    __builtin_nontemporal_store(r, reinterpret_cast<sh_v4*>(p));
+#else
+    *p = v;
+#endif
+}
+
 struct ShRow {
     float v[48];
     __device__ __forceinline__ void load(const float* p, int M, int ncoef) {
@@ -235,7 +262,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
         for (int r = 0; r < 6; ++r) {
             const int f = lane + 64 * r;
             const int row = f / 12;
-            shv[r] = (wbase + row < s.P) ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+            shv[r] = (wbase + row < s.P) ? sh_ld(src + f) : make_float4(0.f, 0.f, 0.f, 0.f);
         }
     }
 
@@ -295,7 +322,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
 #pragma unroll
                     for (int r = 0; r < 6; ++r) {
                         const int f = lane + 64 * r;
-                        shv[r] = (g0 + f / 12 < s.P) ? src[f] : make_float4(0.f, 0.f, 0.f, 0.f);
+                        shv[r] = (g0 + f / 12 < s.P) ? sh_ld(src + f) : make_float4(0.f, 0.f, 0.f, 0.f);
                     }
                 }
 #pragma unroll
@@ -683,7 +710,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
             for (int r = 0; r < 3; ++r) {
                 const int f = lane + 64 * r;  // float4 index in the 16-row run
                 const int row = f / 12, col = f - 12 * (f / 12);
-                if (g0 + row < s.P) dst[f] = srow[wave][row][col];
+                if (g0 + row < s.P) sh_st(dst + f, srow[wave][row][col]);
             }
             __syncthreads();
         }
