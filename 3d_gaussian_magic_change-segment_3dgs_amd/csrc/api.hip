@@ -187,8 +187,13 @@ const char* gsr_last_error(void) { return g_last_error.c_str(); }
 
 const char* gsr_version(void) { return "gsr 0.1 (gfx950)"; }
 
+static bool g_speculate = getenv("GSR_SPECULATE") == nullptr || getenv("GSR_SPECULATE")[0] != '0';
 int gsr_set_option(const char* name, long long value) {
     if (!name) return fail("[gsr] option name is NULL");
+    if (std::string(name) == "speculate") {  // gsr_forward's speculative stage B (default on)
+        g_speculate = value != 0;
+        return 0;
+    }
     if (std::string(name) == "sort_lookback_max") {
         gsr::set_sort_lookback_max(value < 0 ? 0 : (size_t)value);
         return 0;
@@ -199,13 +204,42 @@ int gsr_set_option(const char* name, long long value) {
 
 size_t gsr_geom_bytes(int P) { return gsr::geom_layout(P > 0 ? (size_t)P : 0).bytes; }
 size_t gsr_binning_bytes(int num_rendered) { return gsr::bin_layout(num_rendered > 0 ? (size_t)num_rendered : 0).bytes; }
+int gsr_binning_capacity(size_t bytes) {
+    // largest C with gsr_binning_bytes(C) <= bytes (gsr_binning_bytes is non-decreasing)
+    if (bytes < gsr_binning_bytes(0)) return -1;
+    int lo = 0, hi = 0x7FFFFFFF;
+    while (lo < hi) {
+        const int mid = lo + (hi - lo + 1) / 2;
+        if (gsr_binning_bytes(mid) <= bytes) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
 size_t gsr_img_bytes(int W, int H) { return gsr::img_layout(W, H).bytes; }
 size_t gsr_backward_scratch_bytes(int num_rendered) {
     return gsr::scratch_bytes(num_rendered > 0 ? (size_t)num_rendered : 0);
 }
 
+namespace {
+// Layout capacity (instances) of a binning buffer: settings.binning_capacity if the caller
+// laid the buffer out for more instances than num_rendered (gsr.h), else num_rendered.
+size_t bin_cap(const gsr_settings* s, size_t I) {
+    return s->binning_capacity > 0 && (size_t)s->binning_capacity > I ? (size_t)s->binning_capacity : I;
+}
+int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* stream,
+                  int* num_rendered, bool wait);
+int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* binning, void* img, size_t cap,
+                size_t n_host, const uint32_t* n_dev, float* out_color, float* out_depth, float* out_alpha,
+                float* out_segment, void* stream);
+}  // namespace
+
 int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* stream,
                          int* num_rendered) {
+    return geometry_impl(s, in, geom, radii, stream, num_rendered, true);
+}
+
+namespace {
+int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* stream,
+                  int* num_rendered, bool wait) {
     using namespace gsr;
     g_last_error.clear();
     if (int rc = validate(s, in, true)) return rc;
@@ -255,24 +289,39 @@ int gsr_forward_geometry(const gsr_settings* s, const gsr_inputs* in, void* geom
                                          hs.dev);
     }
     GSR_STAGE("scan");
+    if (!wait) return 0;  // gsr_forward's speculative stage B: waits after launching it
     uint32_t total = 0;
     if (int rc = wait_total(hslot, st, at<uint32_t>(g, L.offsets) + (P - 1), &total)) return rc;
     if (total > 0x7FFFFFFFu) return fail("[gsr] num_rendered overflows int32");
     *num_rendered = (int)total;
     return 0;
 }
+}  // namespace
 
 int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, void* binning, void* img,
                        int num_rendered, float* out_color, float* out_depth, float* out_alpha, float* out_segment,
                        void* stream) {
-    using namespace gsr;
     g_last_error.clear();
+    const size_t I = num_rendered > 0 ? (size_t)num_rendered : 0;
     if (int rc = validate(s, in, true)) return rc;
+    return render_impl(s, in, geom, binning, img, bin_cap(s, I), I, nullptr, out_color, out_depth, out_alpha,
+                       out_segment, stream);
+}
+
+namespace {
+// Stage B.  cap: the binning buffer's layout capacity; n_host: instances to sort (grid
+// sizes); n_dev: when non-NULL, the device word holding num_rendered (speculative stage
+// B, launched before the host knows it: the kernels clamp to min(*n_dev, n_host) and
+// never write a slot >= cap).
+int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* binning, void* img, size_t cap,
+                size_t n_host, const uint32_t* n_dev, float* out_color, float* out_depth, float* out_alpha,
+                float* out_segment, void* stream) {
+    using namespace gsr;
     if (!img || !out_color || !out_depth || !out_alpha || !out_segment) return fail("[gsr] null output buffer");
     hipStream_t st = (hipStream_t)stream;
     const bool dbg = s->debug != 0;
     const int P = s->P;
-    const size_t I = num_rendered > 0 ? (size_t)num_rendered : 0;
+    const size_t I = n_host;
     const ImgLayout IL = img_layout(s->W, s->H);
     const int T = IL.gx * IL.gy;
     char* im = aligned_base(img);
@@ -281,7 +330,7 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
         return fail("[gsr] memset ranges");  // otherwise k_duplicate clears them
     const GeomLayout GL = geom_layout(P > 0 ? P : 0);
     char* g = P > 0 ? aligned_base(geom) : nullptr;
-    const BinLayout BL = bin_layout(I);
+    const BinLayout BL = bin_layout(cap);
     char* b = I > 0 ? aligned_base(binning) : nullptr;
     uint32_t* point_list = nullptr;
     if (I > 0) {
@@ -292,7 +341,7 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
                              at<uint32_t>(g, GL.tiles_touched), at<ushort4>(g, GL.rect),
                              rect_packable(IL.gx, IL.gy) ? at<uint32_t>(g, GL.rect32_sorted) : nullptr, IL.gx,
                              at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid), at<uint32_t>(g, GL.goff),
-                             ranges, T, st);
+                             ranges, T, (uint32_t)cap, st);
         }
         GSR_STAGE("duplicate");
         const int bits = (int)higher_msb((uint32_t)T);
@@ -312,7 +361,7 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
             launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout, at<uint32_t>(b, BL.slot_vals),
                               I, bits, b + BL.ws, /*ws_zeroed=*/false, st,
                               at<uint32_t>(b, BL.slot_gid), at<uint32_t>(b, BL.gid_alt),
-                              at<uint32_t>(b, BL.point_list), &fin);
+                              at<uint32_t>(b, BL.point_list), &fin, /*skip_sentinel=*/false, n_dev);
         }
         GSR_STAGE("tile sort");
         point_list = at<uint32_t>(b, BL.point_list);
@@ -332,10 +381,29 @@ int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void* geom, 
     GSR_STAGE("render");
     return 0;
 }
+}  // namespace
 
 int gsr_forward(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* binning,
                 size_t binning_bytes, void* img, float* out_color, float* out_depth, float* out_alpha,
                 float* out_segment, void* stream, int* num_rendered) {
+    using namespace gsr;
+    const size_t C = s && s->binning_capacity > 0 ? (size_t)s->binning_capacity : 0;
+    if (g_speculate && C > 0 && s->P > 0 && binning && gsr_binning_bytes((int)C) <= binning_bytes) {
+        // Speculative stage B: launched right behind stage A into the caller's buffer laid out
+        // for C instances, the kernels reading num_rendered from device memory; the host waits
+        // for num_rendered only afterwards, so no host round trip stalls the GPU.
+        if (int rc = geometry_impl(s, in, geom, radii, stream, num_rendered, false)) return rc;
+        const GeomLayout L = geom_layout((size_t)s->P);
+        const uint32_t* n_dev = at<uint32_t>(aligned_base(geom), L.offsets) + (s->P - 1);
+        if (int rc = render_impl(s, in, geom, binning, img, C, C, n_dev, out_color, out_depth, out_alpha,
+                                 out_segment, stream))
+            return rc;
+        uint32_t total = 0;
+        if (int rc = wait_total(host_total_slot().host, (hipStream_t)stream, n_dev, &total)) return rc;
+        if (total > 0x7FFFFFFFu) return fail("[gsr] num_rendered overflows int32");
+        *num_rendered = (int)total;
+        return total > C ? GSR_NEED_BINNING : 0;  // over capacity: stage B's results are void
+    }
     if (int rc = gsr_forward_geometry(s, in, geom, radii, stream, num_rendered)) return rc;
     if (*num_rendered > 0 && (binning == nullptr || gsr_binning_bytes(*num_rendered) > binning_bytes))
         return GSR_NEED_BINNING;
@@ -366,7 +434,7 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
     uint32_t* written = nullptr;
     if (I > 0) {
         if (!binning || !scratch) return fail("[gsr] binning/scratch buffer is NULL");
-        const BinLayout BL = bin_layout(I);
+        const BinLayout BL = bin_layout(bin_cap(s, I));
         char* b = aligned_base(binning);
         contrib = reinterpret_cast<float*>(aligned_base(scratch));
         written = at<uint32_t>(b, BL.written);  // cleared by the forward's tile sort
@@ -435,7 +503,7 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
         uint32_t* written = nullptr;
         if (I > 0) {
             if (!V.binning || !V.scratch) return fail("[gsr] multiview: binning/scratch buffer is NULL");
-            const BinLayout BL = bin_layout(I);
+            const BinLayout BL = bin_layout(bin_cap(V.s, I));
             char* b = aligned_base(V.binning);
             contrib = reinterpret_cast<float*>(aligned_base(V.scratch));
             written = at<uint32_t>(b, BL.written);
@@ -537,8 +605,8 @@ int gsr_timing_collect(double* ms, long long* counts) {
     return NUM_STAGES;
 }
 
-long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered, void* geom, void* binning,
-                         void* img, void* dst, void* stream) {
+long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered, int binning_capacity,
+                         void* geom, void* binning, void* img, void* dst, void* stream) {
     using namespace gsr;
     g_last_error.clear();
     if (!name || !dst) {
@@ -548,7 +616,7 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
     const std::string n(name);
     const size_t Pz = P > 0 ? (size_t)P : 0, I = num_rendered > 0 ? (size_t)num_rendered : 0;
     const GeomLayout GL = geom_layout(Pz);
-    const BinLayout BL = bin_layout(I);
+    const BinLayout BL = bin_layout(binning_capacity > 0 && (size_t)binning_capacity > I ? (size_t)binning_capacity : I);
     const ImgLayout IL = img_layout(W, H);
     const size_t T = (size_t)IL.gx * IL.gy;
     const char* src = nullptr;

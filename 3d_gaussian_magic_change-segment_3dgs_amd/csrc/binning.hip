@@ -259,10 +259,17 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restric
 // position is irrelevant): span[2p] = max(256 - d), span[2p + 1] = max(d + 1) (zero-
 // initialised words).  A pass whose keys that matter all share one digit is the
 // identity on them and is skipped (k_radix_scatter copies the tile through).
+// Keys per thread of k_radix_hist: fewer, fuller blocks mean fewer global atomics at the
+// end (one per nonzero (pass, digit) per block).
+#ifndef GSR_HIST_ITEMS
+#define GSR_HIST_ITEMS 16
+#endif
+constexpr int HIST_ITEMS = GSR_HIST_ITEMS;
 __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __restrict__ keys, size_t n,
                                                              int passes, int per_pass, int key_bits,
                                                              uint32_t* __restrict__ hist, uint32_t* span,
-                                                             int skip_sentinel) {
+                                                             int skip_sentinel, const uint32_t* n_dev) {
+    if (n_dev) n = min(n, (size_t)*n_dev);
     __shared__ uint32_t cnt[4][RADIX];
     __shared__ uint32_t s_span[8];
 #pragma unroll
@@ -272,7 +279,6 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __r
     uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};  // max(256 - d), max(d + 1)
     // HIST_ITEMS keys per thread, all loads issued before any use (a strided loop with
     // one dependent load per iteration is latency-bound).
-    constexpr int HIST_ITEMS = 16;
     const size_t base = (size_t)blockIdx.x * SORT_THREADS * HIST_ITEMS + threadIdx.x;
     uint32_t kk[HIST_ITEMS];
 #pragma unroll
@@ -331,7 +337,8 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __r
 template <int ITEMS, int WAVES>
 __global__ void __launch_bounds__(64 * WAVES) k_radix_upsweep(const uint32_t* __restrict__ keys, size_t n,
                                                               int shift, int bits, uint32_t* __restrict__ hist,
-                                                              void* scan_ws, size_t scan_ws16) {
+                                                              void* scan_ws, size_t scan_ws16, const uint32_t* n_dev) {
+    if (n_dev) n = min(n, (size_t)*n_dev);
     constexpr int NT = 64 * WAVES;
     __shared__ uint32_t cnt[RADIX];
     zero16(scan_ws, scan_ws16, (size_t)blockIdx.x * NT + threadIdx.x, (size_t)gridDim.x * NT);
@@ -378,8 +385,9 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
     const uint32_t* __restrict__ keys_in, const uint32_t* __restrict__ vals_in, uint32_t* __restrict__ keys_out,
     uint32_t* __restrict__ vals_out, size_t n, int shift, int bits, const uint32_t* __restrict__ hist,
     uint64_t* status, uint32_t* counter, const uint32_t* __restrict__ vals2_in, uint32_t* __restrict__ vals2_out,
-    SortFinal fin, const uint32_t* span) {
+    SortFinal fin, const uint32_t* span, const uint32_t* n_dev) {
     constexpr int NT = 64 * WAVES, TILE = NT * ITEMS;
+    if (n_dev) n = min(n, (size_t)*n_dev);
     for (size_t i = (size_t)blockIdx.x * NT + threadIdx.x; i < fin.zero16; i += (size_t)gridDim.x * NT)
         fin.zero[i] = make_uint4(0u, 0u, 0u, 0u);
     __shared__ uint32_t s_key[TILE], s_val[TILE], s_val2[TILE];
@@ -486,7 +494,8 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
         }
     }
     __syncthreads();
-    const int nvalid = (int)min((size_t)TILE, n - bbase);
+    // 0 for a tile past n (speculative sorts size the grid by capacity, n by the device count)
+    const int nvalid = bbase < n ? (int)min((size_t)TILE, n - bbase) : 0;
     for (int p = tid; p < nvalid; p += NT) {
         const uint32_t k = s_key[p];
         const uint32_t d = (k >> shift) & mask;
@@ -517,7 +526,8 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
                                                    const ushort4* __restrict__ rect,
                                                    const uint32_t* __restrict__ rect_sorted, int gx,
                                                    uint32_t* __restrict__ tkeys, uint32_t* __restrict__ slot_gid,
-                                                   uint32_t* __restrict__ goff, uint2* __restrict__ ranges, int T) {
+                                                   uint32_t* __restrict__ goff, uint2* __restrict__ ranges, int T,
+                                                   uint32_t cap) {
     __shared__ uint32_t s_key[DUP_CAP], s_gid[DUP_CAP];
     // ranges start at {~0u, 0} for the tile sort's atomicMin / atomicMax; empty tiles end
     // up {0, 0} (rasterizer_impl.cu:316 memset) in k_tile_order
@@ -527,8 +537,11 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
     const int r = r0 + threadIdx.x;
     const int rl = min(r0 + (int)blockDim.x, P) - 1;
     const uint32_t bbase = r0 == 0 ? 0u : offsets[r0 - 1];
-    const uint32_t bend = offsets[rl];
-    const bool staged = bend - bbase <= (uint32_t)DUP_CAP;
+    // cap: slots the binning buffer holds; a speculative launch (gsr_forward) may see more
+    // instances than that, and then writes none past it (the host re-runs this stage)
+    const uint32_t bend_full = offsets[rl];
+    const bool staged = bend_full - bbase <= (uint32_t)DUP_CAP;
+    const uint32_t bend = min(bend_full, max(cap, bbase));
     if (r < P) {
         const uint32_t g = order[r];
         // packed rect in depth order (coalesced) when available, else gathered by id
@@ -555,6 +568,7 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
             } else {
                 for (int y = rc.y; y < rc.w; ++y)
                     for (int x = rc.x; x < rc.z; ++x, ++off) {
+                        if (off >= cap) break;
                         tkeys[off] = (uint32_t)(y * gx + x);
                         slot_gid[off] = g;
                     }
@@ -660,11 +674,11 @@ template <int ITEMS, int WAVES, bool LB>
 static void launch_scatter(size_t n, const uint32_t* kin, const uint32_t* vin, uint32_t* kout, uint32_t* vout,
                            int shift, int bits, const uint32_t* hist, uint64_t* status, uint32_t* counter,
                            const uint32_t* v2in, uint32_t* v2out, SortFinal fin, const uint32_t* span,
-                           hipStream_t st) {
+                           const uint32_t* n_dev, hipStream_t st) {
     static_assert(WAVES * ITEMS % 4 == 0, "tile must be a multiple of 256 elements");
     hipLaunchKernelGGL((k_radix_scatter<ITEMS, WAVES, LB>), dim3(sort_tiles(n, WAVES * ITEMS / 4)),
                        dim3(64 * WAVES), 0, st, kin, vin, kout, vout, n, shift, bits, hist, status, counter, v2in,
-                       v2out, fin, span);
+                       v2out, fin, span, n_dev);
 }
 
 // Stable LSD sort of (keys, vals[, vals2]) on the low key_bits bits.  Ping-pongs
@@ -673,7 +687,7 @@ static void launch_scatter(size_t n, const uint32_t* kin, const uint32_t* vin, u
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_t* keys_tmp, uint32_t* vals_tmp,
                        uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits, void* ws, bool ws_zeroed,
                        hipStream_t st, const uint32_t* vals2_in, uint32_t* vals2_tmp, uint32_t* vals2_out,
-                       const SortFinal* final_out, bool skip_sentinel) {
+                       const SortFinal* final_out, bool skip_sentinel, const uint32_t* n_dev) {
     if (n == 0) return;
     if (key_bits < 1) key_bits = 1;
     const int passes = (key_bits + RADIX_BITS - 1) / RADIX_BITS;
@@ -683,8 +697,8 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     if (lb) {
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);
-        hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)cdiv(n, (size_t)SORT_THREADS * 16)), dim3(SORT_THREADS), 0, st, keys_in,
-                           n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel);
+        hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)cdiv(n, (size_t)SORT_THREADS * HIST_ITEMS)), dim3(SORT_THREADS), 0, st, keys_in,
+                           n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel, n_dev);
     }
     const uint32_t* kin = keys_in;
     const uint32_t* vin = vals_in;
@@ -705,18 +719,18 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
             launch_scatter<GSR_LB_ITEMS, GSR_LB_WAVES, true>(n, kin, vin, kout, vout, shift, bits,
                                                              W.hist + p * RADIX, W.status + (size_t)p * nt * RADIX,
                                                              W.counter + p, v2in, v2out, fin,
-                                                             W.counter + SPAN_WORD + 2 * p, st);
+                                                             W.counter + SPAN_WORD + 2 * p, n_dev, st);
         } else {
             const size_t nt = sort_tiles(n, GSR_TB_ITEMS * GSR_TB_WAVES / 4);
             const size_t len = ((size_t)1 << bits) * nt;
             const ScanWs S = scan_ws(len, W.scan);
             hipLaunchKernelGGL((k_radix_upsweep<GSR_TB_ITEMS, GSR_TB_WAVES>), dim3(nt), dim3(64 * GSR_TB_WAVES), 0, st,
                                kin, n, shift,
-                               bits, W.table, S.base, cdiv(S.bytes, 16));
+                               bits, W.table, S.base, cdiv(S.bytes, 16), n_dev);
             hipLaunchKernelGGL(k_scan<false>, dim3(cdiv(len, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, W.table,
                                nullptr, len, W.table, S.status, S.counter, nullptr, 0);
             launch_scatter<GSR_TB_ITEMS, GSR_TB_WAVES, false>(n, kin, vin, kout, vout, shift, bits, W.table, nullptr,
-                                                              nullptr, v2in, v2out, fin, nullptr, st);
+                                                              nullptr, v2in, v2out, fin, nullptr, n_dev, st);
         }
         kin = kout;
         vin = vout;
@@ -731,10 +745,10 @@ void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st) {
 
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, const uint32_t* rect_sorted, int gx, uint32_t* tkeys,
-                      uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, hipStream_t st) {
+                      uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, uint32_t cap, hipStream_t st) {
     if (P == 0) return;
     hipLaunchKernelGGL(k_duplicate, dim3(cdiv(P, 256)), dim3(256), 0, st, P, order, offsets, tiles_touched, rect,
-                       rect_sorted, gx, tkeys, slot_gid, goff, ranges, T);
+                       rect_sorted, gx, tkeys, slot_gid, goff, ranges, T, cap);
 }
 
 

@@ -224,7 +224,8 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL =
                        uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,
                        void* ws, bool ws_zeroed, hipStream_t st, const uint32_t* vals2_in = nullptr,
                        uint32_t* vals2_tmp = nullptr, uint32_t* vals2_out = nullptr, const SortFinal* fin = nullptr,
-                       bool skip_sentinel = false);
+                       bool skip_sentinel = false, const uint32_t* n_dev = nullptr);
+// n_dev: optional device word; the sort then covers min(*n_dev, n) keys (n sizes the grids)
 int depth_sort_passes();
 int sort_lb_items();
 bool sort_uses_lookback(size_t n);
@@ -237,7 +238,7 @@ void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_id
                                   bool rect_mode = false);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, const uint32_t* rect_sorted, int gx, uint32_t* tkeys,
-                      uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, hipStream_t st);
+                      uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, uint32_t cap, hipStream_t st);
 // render.hip
 void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
                            const uint32_t* point_list,

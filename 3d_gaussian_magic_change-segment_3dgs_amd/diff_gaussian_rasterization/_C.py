@@ -7,6 +7,7 @@ The product path is libgsr.so only: if it is missing, importing this module
 raises ImportError -- there is no CPU or PyTorch fallback.
 """
 import ctypes
+import functools
 import os
 
 import torch  # must be imported first: libgsr.so binds to torch's HIP runtime (same soname)
@@ -32,7 +33,7 @@ class _Settings(ctypes.Structure):
         ("tanfovx", ctypes.c_float), ("tanfovy", ctypes.c_float), ("scale_modifier", ctypes.c_float),
         ("prefiltered", ctypes.c_int), ("debug", ctypes.c_int),
         ("bg", ctypes.c_void_p), ("viewmatrix", ctypes.c_void_p), ("projmatrix", ctypes.c_void_p),
-        ("campos", ctypes.c_void_p),
+        ("campos", ctypes.c_void_p), ("binning_capacity", ctypes.c_int),
     ]
 
 
@@ -51,6 +52,8 @@ _lib.gsr_geom_bytes.restype = _sz
 _lib.gsr_geom_bytes.argtypes = [_i]
 _lib.gsr_binning_bytes.restype = _sz
 _lib.gsr_binning_bytes.argtypes = [_i]
+_lib.gsr_binning_capacity.restype = _i
+_lib.gsr_binning_capacity.argtypes = [_sz]
 _lib.gsr_img_bytes.restype = _sz
 _lib.gsr_img_bytes.argtypes = [_i, _i]
 _lib.gsr_backward_scratch_bytes.restype = _sz
@@ -73,7 +76,7 @@ _lib.gsr_mark_visible.argtypes = [_i, _vp, _vp, _vp, _vp, _vp]
 _lib.gsr_last_error.restype = ctypes.c_char_p
 _lib.gsr_version.restype = ctypes.c_char_p
 _lib.gsr_debug_copy.restype = ctypes.c_longlong
-_lib.gsr_debug_copy.argtypes = [ctypes.c_char_p, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]
+_lib.gsr_debug_copy.argtypes = [ctypes.c_char_p, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp]
 
 class _ViewState(ctypes.Structure):
     _fields_ = [("s", ctypes.POINTER(_Settings)), ("radii", ctypes.c_void_p), ("geom", ctypes.c_void_p),
@@ -112,7 +115,7 @@ _lib.gsr_timing_enable.argtypes = [_i]
 _lib.gsr_timing_collect.restype = _i
 _lib.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
 
-EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_img_bytes", "gsr_backward_scratch_bytes",
+EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_binning_capacity", "gsr_img_bytes", "gsr_backward_scratch_bytes",
                     "gsr_forward_geometry", "gsr_forward_render", "gsr_forward", "gsr_backward", "gsr_mark_visible",
                     "gsr_debug_copy", "gsr_num_stages", "gsr_stage_name", "gsr_timing_enable", "gsr_timing_collect",
                     "gsr_last_error", "gsr_version", "gsr_set_option", "gsr_multiview_scratch_bytes",
@@ -135,11 +138,19 @@ def debug_state(name, P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffe
     dev = geomBuffer.device
     out = torch.empty(max(n, 1), dtype=dtype, device=dev)
     ptr = lambda t: t.data_ptr() if t is not None and t.numel() else None
-    rc = _lib.gsr_debug_copy(name.encode(), P, W, H, num_rendered, ptr(geomBuffer), ptr(binningBuffer),
-                             ptr(imgBuffer), out.data_ptr(), _stream(dev))
+    rc = _lib.gsr_debug_copy(name.encode(), P, W, H, num_rendered, binning_capacity(binningBuffer),
+                             ptr(geomBuffer), ptr(binningBuffer), ptr(imgBuffer), out.data_ptr(), _stream(dev))
     if rc < 0:
         raise RuntimeError(f"gsr_debug_copy({name}) failed: {_lib.gsr_last_error().decode()}")
     return out[:n]
+
+
+def binning_capacity(binning):
+    """Layout capacity (instances) of a binning buffer allocated as gsr_binning_bytes(C)
+    (gsr_settings.binning_capacity; 0 for an empty buffer)."""
+    if binning is None or binning.numel() == 0:
+        return 0
+    return max(0, int(_lib.gsr_binning_capacity(binning.numel())))
 
 
 def version():
@@ -258,6 +269,9 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
         cap = _last_rendered.get(device, 0)
         cap = cap + cap // 7 + 4096 if cap and _BIN_GUESS else 0
         binning = torch.empty(_lib.gsr_binning_bytes(cap), **u8) if cap else None
+        # every call on a binning buffer uses the layout of its capacity (gsr.h); with a guess
+        # gsr_forward runs stage B speculatively right behind stage A
+        s.binning_capacity = binning_capacity(binning)
         nr = ctypes.c_int(0)
         # geometry, the num_rendered sync and the render in one C call when the guess holds
         rc = _lib.gsr_forward(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), radii.data_ptr(),
@@ -268,6 +282,7 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
         _last_rendered[device] = num_rendered
         if rc == GSR_NEED_BINNING:  # no guess, or too small: stage B with the exact size
             binning = torch.empty(_lib.gsr_binning_bytes(num_rendered), **u8)
+            s.binning_capacity = binning_capacity(binning)
             rc = _lib.gsr_forward_render(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), binning.data_ptr(),
                                          img.data_ptr(), num_rendered, color.data_ptr(), depth.data_ptr(),
                                          alpha.data_ptr(), segment.data_ptr(), stream)
@@ -282,6 +297,7 @@ def set_option(name, value):
     _check(_lib.gsr_set_option(name.encode(), int(value)))
 
 
+@functools.lru_cache(maxsize=64)
 def grad_arena_layout(P, M):
     """Offsets (in floats) of the gradients inside the single arena allocated by
     rasterize_gaussians_backward.  The first `bucket` floats are the parameter
@@ -343,6 +359,7 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, segments, s
         campos_ = _dev_f32(campos, device, "campos")
         s = _settings(P, int(degree), M, W, H, tan_fovx, tan_fovy, scale_modifier, False, debug, bg_, view_, proj_,
                       campos_)
+        s.binning_capacity = binning_capacity(binningBuffer)
         inp = _inputs(means3D_, sh_, colors_, segments_, None, scales_, rotations_, cov_)  # opacities unused
         ups = [_dev_f32(t, device, n) for t, n in ((dL_dout_color, "dL_dcolor"), (dL_dout_segment, "dL_dsegment"),
                                                    (dL_dout_depth, "dL_ddepth"), (dL_dout_alpha, "dL_dalpha"))]
@@ -467,6 +484,7 @@ def rasterize_gaussians_backward_multiview(views, means3D, colors, segments, sca
             cp = _dev_f32(V["campos"], device, "campos")
             st = _settings(P, int(degree), M, W, H, V["tanfovx"], V["tanfovy"], scale_modifier, False, debug, bg_,
                            vm, pm, cp)
+            st.binning_capacity = binning_capacity(V["binning"])
             ups = [_dev_f32(V[n], device, n) for n in ("dL_dcolor", "dL_dsegment", "dL_ddepth", "dL_dalpha")]
             ups = [u if u is not None else torch.zeros(c, H, W, **f32)
                    for u, c in zip(ups, (NUM_CHANNELS, NUM_CLASS, 1, 1))]

@@ -65,6 +65,12 @@ typedef struct gsr_settings {
     const float* viewmatrix; /* device [16], W2C^T row-major (scene/cameras.py:58) */
     const float* projmatrix; /* device [16], viewmatrix @ proj^T (scene/cameras.py:60) */
     const float* campos;     /* device [3] */
+    /* Instances the binning buffer is laid out for; 0 = num_rendered.  gsr_forward with
+     * binning_capacity = C > 0 (and a buffer of gsr_binning_bytes(C)) runs stage B before
+     * num_rendered reaches the host; every later call on that buffer (gsr_backward,
+     * gsr_backward_multiview, gsr_debug_copy) passes the same C.  For a buffer of exactly
+     * gsr_binning_bytes(num_rendered), gsr_binning_capacity(size) is equivalent to 0. */
+    int binning_capacity;
 } gsr_settings;
 
 /* Per-Gaussian inputs (device pointers, NULL = absent). */
@@ -100,6 +106,9 @@ typedef struct gsr_grads {
  * for the same arguments. */
 GSR_API size_t gsr_geom_bytes(int P);
 GSR_API size_t gsr_binning_bytes(int num_rendered);
+/* largest C with gsr_binning_bytes(C) <= bytes (-1 if none): the layout capacity of a binning
+ * buffer of that size (settings.binning_capacity) */
+GSR_API int gsr_binning_capacity(size_t bytes);
 GSR_API size_t gsr_img_bytes(int W, int H);
 /* scratch needed by gsr_backward (per-instance gradient records) */
 GSR_API size_t gsr_backward_scratch_bytes(int num_rendered);
@@ -124,7 +133,11 @@ GSR_API int gsr_forward_render(const gsr_settings* s, const gsr_inputs* in, void
  * 198-344): stage A, the num_rendered sync, then stage B straight from C when the
  * caller's binning buffer (binning_bytes, e.g. a guess from the previous view) holds
  * gsr_binning_bytes(num_rendered) -- no host-language round trip sits between the
- * sync and the render launches.  Returns 0 (rendered), GSR_NEED_BINNING (stage A done,
+ * sync and the render launches.  With s->binning_capacity = C > 0 and binning_bytes >=
+ * gsr_binning_bytes(C), stage B is launched right behind stage A, before num_rendered
+ * reaches the host (its kernels read it on the device and write nothing past C); the
+ * host waits only afterwards.  If num_rendered turns out > C, stage B's outputs are void
+ * and GSR_NEED_BINNING is returned.  Returns 0 (rendered), GSR_NEED_BINNING (stage A done,
  * *num_rendered set, nothing rendered: call gsr_forward_render with a buffer of
  * gsr_binning_bytes(*num_rendered)), or another nonzero error (gsr_last_error). */
 #define GSR_NEED_BINNING 2
@@ -208,8 +221,8 @@ GSR_API int gsr_mark_visible(int P, const float* means3D, const float* viewmatri
  * "goff" u32[P], "point_list" u32[I], "slot_vals" u32[I], "ranges" u32[T,2],
  * "n_contrib_tiles" u32[T,256] (tile-major, entry k*64+l = pixel
  * (16*tx + (l&15), 16*ty + (l>>4) + 4k)).  Returns the byte count copied, or -1. */
-GSR_API long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered, void* geom,
-                                 void* binning, void* img, void* dst, void* stream);
+GSR_API long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered, int binning_capacity,
+                                 void* geom, void* binning, void* img, void* dst, void* stream);
 
 /* ---- live stage timing (bench/profiling): gsr_timing_enable(mask) brackets every
  * stage i with (mask >> i) & 1 set (mask -1 = all, 0 = off) by hipEvents recorded

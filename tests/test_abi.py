@@ -100,7 +100,7 @@ def test_errors_reported_without_touching_the_device():
     inp.scales, inp.rotations = 16, 32
     rc = L.gsr_forward_geometry(ctypes.byref(s), ctypes.byref(inp), None, None, None, ctypes.byref(nr))
     assert rc != 0 and b"SH degree" in L.gsr_last_error()
-    assert L.gsr_debug_copy(b"no_such_field", 1, 16, 16, 0, None, None, None, 16, None) == -1
+    assert L.gsr_debug_copy(b"no_such_field", 1, 16, 16, 0, 0, None, None, None, 16, None) == -1
 
 
 def test_python_api_rejects_cpu_tensors():

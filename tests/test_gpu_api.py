@@ -136,3 +136,40 @@ def test_loss_on_colour_only(gpu_available):
 
     for a, b in zip(run(False), run(True)):
         torch.testing.assert_close(a, b, rtol=0, atol=0)
+
+
+def _outputs_and_grads(scene, cam):
+    img, radii, ssp, params, _ = _renderer_style_call(scene, cam)
+    out = {"img": img.detach().clone(), "radii": radii.clone(), "ssp": ssp.grad.clone()}
+    out.update({n: p.grad.clone() for n, p in params.items()})
+    return out
+
+
+def test_speculative_stage_b_matches_exact(gpu_available):
+    """gsr_forward with a binning-capacity guess launches stage B before num_rendered
+    reaches the host (gsr.h).  It must give bit-identical images and gradients to the
+    exact path, both when the guess holds and when it is too small (GSR_NEED_BINNING ->
+    stage B re-run with the exact buffer)."""
+    from diff_gaussian_rasterization import _C
+    small = synthetic_scene(800, sh_degree=3, seed=31)
+    big = synthetic_scene(6000, sh_degree=3, seed=32)
+    cam = orbit_camera(2, 176, 128, 160.0)
+    saved = dict(_C._last_rendered)
+    try:
+        _C.set_option("speculate", 0)
+        _C._last_rendered.clear()
+        ref_big = _outputs_and_grads(big, cam)     # exact path (no guess)
+        ref_small = _outputs_and_grads(small, cam)  # guess buffer from big, stage B after the sync
+        _C.set_option("speculate", 1)
+        _C._last_rendered.clear()
+        _outputs_and_grads(small, cam)             # sets the guess from the small scene
+        spec_big = _outputs_and_grads(big, cam)    # guess too small: NEED_BINNING fallback
+        spec_big2 = _outputs_and_grads(big, cam)   # guess from big: speculative stage B holds
+        spec_small = _outputs_and_grads(small, cam)  # capacity far above num_rendered
+    finally:
+        _C.set_option("speculate", 1)
+        _C._last_rendered.clear()
+        _C._last_rendered.update(saved)
+    for got, ref in ((spec_big, ref_big), (spec_big2, ref_big), (spec_small, ref_small)):
+        for k in ref:
+            assert torch.equal(got[k], ref[k]), k
