@@ -134,3 +134,18 @@ def test_grad_arena_layout_bucket_first():
             assert lay[a][0] + lay[a][1] * P <= lay[b][0]
         assert lay["dsegments"][0] + 2 * P <= total < lay["dsegments"][0] + 2 * P + 64
         assert lay["dmeans2D"][0] == total and lay["total"][1] >= lay["dcov3D"][0] + 6 * P
+
+
+def test_binning_capacity_inverts_the_size_query():
+    """gsr_binning_capacity(bytes) is the largest C with gsr_binning_bytes(C) <= bytes: the
+    layout capacity every call derives from a binning buffer's size (gsr.h)."""
+    from diff_gaussian_rasterization import _C
+    L = _C._lib
+    assert L.gsr_binning_capacity(0) == -1
+    for I in (0, 1, 63, 64, 4095, 4096, 100_000, 8_015_689, 9_218_042):
+        b = L.gsr_binning_bytes(I)
+        C = L.gsr_binning_capacity(b)
+        assert C >= I and L.gsr_binning_bytes(C) == b and L.gsr_binning_bytes(C + 1) > b
+        assert L.gsr_binning_capacity(b - 1) < I or I == 0
+    t = torch.empty(L.gsr_binning_bytes(5000), dtype=torch.uint8)
+    assert _C.binning_capacity(t) >= 5000 and _C.binning_capacity(torch.empty(0, dtype=torch.uint8)) == 0
