@@ -242,13 +242,6 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     const int sidx = live ? idx : 0;
     Cam cam;
     load_cam(s, cam);
-    if (live) {
-        radii[idx] = 0;
-        tiles_touched[idx] = 0;
-        depth_keys[idx] = 0xFFFFFFFFu;  // culled Gaussians sort last; they emit no instances
-        clamped[idx] = 0;
-        if (rect32) rect32[idx] = 0u;   // empty rect: no tiles
-    }
 
     // SH3 rows through LDS (below): the first half-run's loads are issued before the
     // projection math so their latency overlaps it.
@@ -348,7 +341,16 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     } else if (ok) {
         rgb = ld3(in.colors_precomp + 3 * (size_t)idx);
     }
-    if (!ok) return;
+    if (!ok) {  // culled (the reference's early returns): no tiles, sorted last
+        if (live) {
+            radii[idx] = 0;
+            tiles_touched[idx] = 0;
+            depth_keys[idx] = 0xFFFFFFFFu;  // culled Gaussians sort last; they emit no instances
+            clamped[idx] = 0;
+            if (rect32) rect32[idx] = 0u;   // empty rect: no tiles
+        }
+        return;
+    }
     float s0 = 0.f, s1 = 0.f;
     if (in.segments) {
         const float2 sg = *reinterpret_cast<const float2*>(in.segments + 2 * (size_t)idx);
@@ -364,7 +366,8 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     tiles_touched[idx] = ntiles;
     depth_keys[idx] = __float_as_uint(p_view.z);
     clamped[idx] = cbits;
-    rect[idx] = make_ushort4((unsigned short)x0, (unsigned short)y0, (unsigned short)x1, (unsigned short)y1);
+    if (!rect32)  // the unpacked rect is read only when the packed one is unavailable
+        rect[idx] = make_ushort4((unsigned short)x0, (unsigned short)y0, (unsigned short)x1, (unsigned short)y1);
     if (rect32) rect32[idx] = (uint32_t)x0 | ((uint32_t)y0 << 8) | ((uint32_t)x1 << 16) | ((uint32_t)y1 << 24);
 }
 
