@@ -270,11 +270,12 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
     {
         // Depth order: 32-bit keys -> 4 passes (even: sorted keys land back in depth_keys).
         StageScope sc(GSR_STAGE_DEPTH_SORT, st);
+        const SortFinal nokeys{nullptr, nullptr, 0, true};  // only the order (+ rects) is used
         launch_radix_sort(at<uint32_t>(g, L.depth_keys), nullptr, at<uint32_t>(g, L.dkeys_alt),
                           at<uint32_t>(g, L.order_alt), at<uint32_t>(g, L.depth_keys), at<uint32_t>(g, L.order), P,
                           32, g + L.ws, /*ws_zeroed=*/true, st, packed ? at<uint32_t>(g, L.rect32) : nullptr,
                           packed ? at<uint32_t>(g, L.rect32_alt) : nullptr,
-                          packed ? at<uint32_t>(g, L.rect32_sorted) : nullptr, nullptr,
+                          packed ? at<uint32_t>(g, L.rect32_sorted) : nullptr, &nokeys,
                           /*skip_sentinel=*/true);  // culled Gaussians (key ~0u) emit nothing
     }
     GSR_STAGE("depth sort");

@@ -712,8 +712,8 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
         uint32_t* vout = to_out ? vals_out : vals_tmp;
         uint32_t* v2out = vals2_in ? (to_out ? vals2_out : vals2_tmp) : nullptr;
         const bool last = p == passes - 1;
-        const SortFinal fin = (last && final_out) ? *final_out : SortFinal{nullptr, nullptr, 0};
-        if (fin.ranges) kout = nullptr;  // the ranges replace the sorted keys
+        const SortFinal fin = (last && final_out) ? *final_out : SortFinal{nullptr, nullptr, 0, false};
+        if (fin.ranges || fin.no_keys) kout = nullptr;  // the ranges replace the sorted keys
         if (lb) {
             const size_t nt = sort_tiles(n, sort_lb_items());
             launch_scatter<GSR_LB_ITEMS, GSR_LB_WAVES, true>(n, kin, vin, kout, vout, shift, bits,

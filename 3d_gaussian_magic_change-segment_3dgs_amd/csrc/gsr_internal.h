@@ -219,6 +219,7 @@ struct SortFinal {
     uint2* ranges;
     uint4* zero;
     size_t zero16;
+    bool no_keys;  // the sorted keys are not needed: the last pass writes none
 };
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL = identity*/, uint32_t* keys_tmp,
                        uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,
