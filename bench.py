@@ -112,7 +112,7 @@ def cpu_baseline(scene, cam, grads, budget_s=20.0):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--steps", type=int, default=200)
     ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="mt", help="gsr_tools.scene.CONFIGS key (default: the metric config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
