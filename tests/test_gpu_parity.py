@@ -206,3 +206,14 @@ def test_table_mode_sorts(gpu_available, oracle_mod):
         compare(oracle_mod, scene, cam)
     finally:
         _C.set_option("sort_lookback_max", 4 << 20)
+
+
+def test_grid_wider_than_packed_rect(gpu_available, oracle_mod):
+    """More than 255 tiles across (4160 px): the tile rect does not fit the packed 8-bit
+    form the depth sort carries, so the scan gathers tiles_touched by depth order and the
+    duplicate reads the ushort4 rect (the general path of DESIGN.md s3)."""
+    scene = synthetic_scene(6000, sh_degree=3, seed=27)
+    cam = make_camera(np.eye(3), np.array([0.0, 0.0, 4.0]), 4160, 48, focal2fov(1200.0, 4160),
+                      focal2fov(1200.0, 48))
+    g, r = compare(oracle_mod, scene, cam)
+    assert g["num_rendered"] > 1000
