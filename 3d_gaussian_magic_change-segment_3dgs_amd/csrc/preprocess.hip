@@ -382,6 +382,35 @@ __global__ void k_mark_visible(int P, const float* __restrict__ means3D, const f
     present[idx] = xform4x3(ld3(means3D + 3 * (size_t)idx), v).z > 0.2f ? 1 : 0;
 }
 
+// Gather-sum of the written instance records of one Gaussian's slot range [lo, hi)
+// (a Gaussian's slots are contiguous), in slot order: deterministic.  The sum runs in
+// fp64 (rounded once at the end): a Gaussian covering hundreds of tiles otherwise adds
+// a sequential fp32 rounding error per tile, which the cov2D backward amplifies by
+// 1/det(cov2D)^2 for elongated Gaussians (C5: dscales off by 1.3e-5 of the tensor max
+// in fp32).  The kernel is HBM-bound; the fp64 adds cost no time.
+__device__ __forceinline__ void sum_records(const float* __restrict__ contrib, const uint32_t* __restrict__ written,
+                                            uint32_t lo, uint32_t hi, float q[12]) {
+    double d[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) d[j] = 0.0;
+    for (uint32_t w = lo >> 5; w <= (hi - 1) >> 5; ++w) {
+        uint32_t bits = written[w];
+        if (w == lo >> 5) bits &= ~0u << (lo & 31);
+        if (w == (hi - 1) >> 5 && ((hi & 31) != 0)) bits &= ~(~0u << (hi & 31));
+        while (bits) {
+            const uint32_t u = (w << 5) + (uint32_t)__builtin_ctz(bits);
+            bits &= bits - 1;
+            const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)u * 12);
+            const float4 a = src[0], b = src[1], c = src[2];
+            d[0] += a.x; d[1] += a.y; d[2] += a.z; d[3] += a.w;
+            d[4] += b.x; d[5] += b.y; d[6] += b.z; d[7] += b.w;
+            d[8] += c.x; d[9] += c.y; d[10] += c.z; d[11] += c.w;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 12; ++j) q[j] = (float)d[j];
+}
+
 // ----------------------------------------------------------------- backward --
 // One thread per Gaussian.  Sums the per-(tile, Gaussian) gradient records that
 // the render backward wrote at the Gaussian's instance slots (replacing the
@@ -434,25 +463,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         // [goff, goff + tiles_touched), in slot order (deterministic).
         const float4 r0 = rec[(size_t)idx * REC_F4], r1 = rec[(size_t)idx * REC_F4 + 1];
         float q[12];
-#pragma unroll
-        for (int j = 0; j < 12; ++j) q[j] = 0.f;
-        {
-            const uint32_t lo = goff[idx], hi = lo + tiles_touched[idx];
-            for (uint32_t w = lo >> 5; w <= (hi - 1) >> 5; ++w) {
-                uint32_t bits = written[w];
-                if (w == lo >> 5) bits &= ~0u << (lo & 31);
-                if (w == (hi - 1) >> 5 && ((hi & 31) != 0)) bits &= ~(~0u << (hi & 31));
-                while (bits) {
-                    const uint32_t u = (w << 5) + (uint32_t)__builtin_ctz(bits);
-                    bits &= bits - 1;
-                    const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)u * 12);
-                    const float4 a = src[0], b = src[1], c = src[2];
-                    q[0] += a.x; q[1] += a.y; q[2] += a.z; q[3] += a.w;
-                    q[4] += b.x; q[5] += b.y; q[6] += b.z; q[7] += b.w;
-                    q[8] += c.x; q[9] += c.y; q[10] += c.z; q[11] += c.w;
-                }
-            }
-        }
+        sum_records(contrib, written, goff[idx], goff[idx] + tiles_touched[idx], q);
         const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
         const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * s.W);
         const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * s.H);
@@ -771,25 +782,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, floa
         }
         const float4 r0 = w.rec[(size_t)idx * REC_F4], r1 = w.rec[(size_t)idx * REC_F4 + 1];
         float q[12];
-#pragma unroll
-        for (int j = 0; j < 12; ++j) q[j] = 0.f;
-        {
-            const uint32_t lo = w.goff[idx], hi = lo + w.tiles_touched[idx];
-            for (uint32_t ww = lo >> 5; ww <= (hi - 1) >> 5; ++ww) {
-                uint32_t bits = w.written[ww];
-                if (ww == lo >> 5) bits &= ~0u << (lo & 31);
-                if (ww == (hi - 1) >> 5 && ((hi & 31) != 0)) bits &= ~(~0u << (hi & 31));
-                while (bits) {
-                    const uint32_t u = (ww << 5) + (uint32_t)__builtin_ctz(bits);
-                    bits &= bits - 1;
-                    const float4* src = reinterpret_cast<const float4*>(w.contrib + (size_t)u * 12);
-                    const float4 x = src[0], y = src[1], z = src[2];
-                    q[0] += x.x; q[1] += x.y; q[2] += x.z; q[3] += x.w;
-                    q[4] += y.x; q[5] += y.y; q[6] += y.z; q[7] += y.w;
-                    q[8] += z.x; q[9] += z.y; q[10] += z.z; q[11] += z.w;
-                }
-            }
-        }
+        sum_records(w.contrib, w.written, w.goff[idx], w.goff[idx] + w.tiles_touched[idx], q);
         const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
         const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * w.W);
         const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * w.H);

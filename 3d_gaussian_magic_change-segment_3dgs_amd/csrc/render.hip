@@ -2,17 +2,21 @@
 // back-to-front replay (backward).  Reference: DGR/cuda_rasterizer/
 // forward.cu:258-392 (renderCUDA) and backward.cu:414-639 (renderCUDA bwd).
 //
-// MI355X mapping: ONE wave64 per 16x16 tile, 4 pixels per lane (lane l owns
-// column l&15 of rows (l>>4) + 4k, k = 0..3).  Per batch of 64 sorted
-// instances each lane fetches one 64-B record with three 16-B loads; the blend
-// loop then broadcasts record j to the wave with v_readlane (scalar operands,
-// no LDS, no block barriers).  Early termination is a wave ballot.
+// MI355X mapping: ONE wave64 per 16x16 tile, 4 pixels per lane.  Forward: lane l
+// owns pixel (l&7, l>>3) of each 8x8 quadrant k of the tile (quadrant-gated);
+// backward: lane l owns column l&15 of rows (l>>4) + 4k, k = 0..3 (16x4 strips, one
+// dx per lane for the moment sums).  Per batch of 64 sorted instances each lane
+// fetches one 64-B record with three 16-B loads (two-stage prefetch); the batch is
+// parked in LDS and the blend loop reads record j with a wave-uniform broadcast
+// ds_read (no v_readlane, no block barriers: one wave per block).  Early
+// termination is tracked as per-quadrant live masks in SGPRs (ballots).
 //
 // Per pair, the four pixel "powers" are computed first and compared with the
 // Gaussian's log-space opacity threshold ln(1/(255*o)) (minus a 1e-3 guard):
 // when no pixel of the tile can reach alpha >= 1/255 the pair is skipped
 // before any exp().  Pairs that pass are decided with the exact test of the
-// reference (expf, alpha >= 1/255), so the skip never changes a result.
+// reference (alpha >= 1/255 with the blend exp below), so the skip never changes a
+// result.
 //
 // Backward: instead of the reference's 12 float atomics per (pixel, Gaussian)
 // pair, each lane sums its 4 pixels in registers, the wave reduces the 12

@@ -326,7 +326,9 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, segments, s
                                  binningBuffer, imageBuffer, alpha, debug):
     """RasterizeGaussiansBackwardCUDA (DGR/rasterize_points.cu:127-221).
     Returns (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
-    dL_drotations, dL_dsegments); gradients of absent (empty) inputs are None."""
+    dL_drotations, dL_dsegments).  Gradients of absent (empty) inputs are zero tensors of the
+    reference's shapes ([P,3] / [P,6] / [P,0,3] / [P,3] / [P,4] / [P,2], rasterize_points.cu:
+    166-177), as read-only stride-0 views of one zero (no memory traffic)."""
     P = int(means3D.size(0))
     shaped = next(t for t in (dL_dout_color, dL_dout_segment, dL_dout_depth, dL_dout_alpha, alpha) if t is not None)
     H, W = int(shaped.size(-2)), int(shaped.size(-1))
@@ -382,10 +384,22 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, segments, s
                                  R, alpha_.data_ptr(), ups[0].data_ptr(), ups[1].data_ptr(), ups[2].data_ptr(),
                                  ups[3].data_ptr(), scratch.data_ptr() if R > 0 else None, ctypes.byref(g),
                                  _stream(device)))
-    return (dmeans2D, dcolors if colors_ is not None else None, dopacity, dmeans3D,
-            dcov3D if cov_ is not None else None, dsh if sh_ is not None else None,
-            dscales if scales_ is not None else None, drot if scales_ is not None else None,
-            dsegments if segments_ is not None else None)
+    Z = lambda *shape: _zeros(device, *shape)
+    return (dmeans2D, dcolors if colors_ is not None else Z(P, 3), dopacity, dmeans3D,
+            dcov3D if cov_ is not None else Z(P, 6), dsh if sh_ is not None else Z(P, 0, 3),
+            dscales if scales_ is not None else Z(P, 3), drot if scales_ is not None else Z(P, 4),
+            dsegments if segments_ is not None else Z(P, NUM_CLASS))
+
+
+_ZERO = {}
+
+
+def _zeros(device, *shape):
+    """A zero-filled [shape] tensor without memory traffic: one cached zero, expanded."""
+    z = _ZERO.get(device)
+    if z is None:
+        z = _ZERO[device] = torch.zeros((), dtype=torch.float32, device=device)
+    return z.expand(*shape)
 
 
 def mark_visible(means3D, viewmatrix, projmatrix):

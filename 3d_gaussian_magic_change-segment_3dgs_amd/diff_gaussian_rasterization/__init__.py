@@ -1,3 +1,19 @@
+#
+# Portions of this file (the public API surface: GaussianRasterizationSettings,
+# GaussianRasterizer, rasterize_gaussians, _RasterizeGaussians -- their argument
+# tuples, validation messages and debug snapshot handling) follow
+# submodules_local/diff-gaussian-rasterization/diff_gaussian_rasterization/__init__.py
+# of the reference, which carries this notice:
+#
+# Copyright (C) 2023, Inria
+# GRAPHDECO research group, https://team.inria.fr/graphdeco
+# All rights reserved.
+#
+# This software is free for non-commercial, research and evaluation use
+# under the terms of the LICENSE.md file.
+#
+# For inquiries contact  george.drettakis@inria.fr
+#
 """diff_gaussian_rasterization -- MI355X-native drop-in for the reference's
 differentiable Gaussian rasterizer (DGR/diff_gaussian_rasterization/__init__.py).
 
@@ -66,7 +82,8 @@ def _backward_views(views, means3D, colors_precomp, segments, scales, rotations,
                                                         sh_rows=rows)
     if rows is not None:
         _, _, _, g_means3D, _, g_sh, _, _, _ = out
-        sink.record(rows, len(views), means3D, sh, sh_degree, g_sh, g_means3D)
+        sink.record(rows, len(views), means3D, sh, sh_degree, g_sh, g_means3D,
+                    inputs=tuple(t for t in (segments, scales, rotations) if isinstance(t, torch.Tensor)))
     return out, d2
 
 

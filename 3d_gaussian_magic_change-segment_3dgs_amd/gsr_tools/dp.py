@@ -113,22 +113,49 @@ class ShExchange:
     Nothing may read the deferred dsh / dmeans3D before h.wait().  On GPU tensors the
     collectives run on the process group's stream and the SH completion on a side
     stream that waits for them; h.wait() orders the caller's stream after it.
+
+    With loss.backward() the parameters' .grad must be the backward's gradient views
+    themselves (autograd hands them over without a copy when .grad is None, i.e. after
+    zero_grad(set_to_none=True), and when the rasterizer inputs are the leaves or
+    gsr_train's arena parameters): the exchange completes them in place.  The recorder
+    therefore keeps no reference to the returned gradient tensors (a reference would
+    make autograd clone them before they are complete).  If autograd did copy or
+    accumulate into a leaf's existing .grad (a .grad that was not None, or a graph
+    between the leaf and the rasterizer that reshapes the gradient), h.wait() raises
+    instead of leaving a gradient computed from unfinished memory.
     `sh_backward` replaces _C.sh_backward (CPU tests pass the oracle's)."""
 
-    def __init__(self, group=None, sh_backward=None):
+    def __init__(self, group=None, sh_backward=None, params=()):
+        """params: further leaf tensors whose .grad comes from the exchanged bucket
+        (e.g. the opacity leaf, which the backward does not see) -- checked at wait()
+        like the rasterizer inputs."""
         self.group = group
         self.entries = []
         self._sh_backward = sh_backward
+        self._params = tuple(params)
 
     # -- called by the deferred backward (diff_gaussian_rasterization._backward_views)
     def sh_rows(self, B, P, device):
         from diff_gaussian_rasterization._C import sh_rows_floats
         return torch.empty(B * sh_rows_floats(P), dtype=torch.float32, device=device)
 
-    def record(self, rows, B, means3D, sh, degree, dsh, dmeans3D):
+    def record(self, rows, B, means3D, sh, degree, dsh, dmeans3D, inputs=()):
         arena = arena_of(dmeans3D)
-        self.entries.append(dict(rows=rows, B=B, means3D=means3D, sh=sh, degree=int(degree), dsh=dsh,
-                                 dmeans3D=dmeans3D, arena=arena))
+        P, M = int(means3D.size(0)), int(sh.size(1))
+        lay = arena_layout(P, M)
+        if dsh.data_ptr() != arena.data_ptr() + 4 * lay["dsh"][0]:
+            raise RuntimeError("deferred dsh is not the dsh block of the gradient arena")
+        # leaves whose .grad autograd fills after this backward returns: remember what
+        # .grad was, to detect at wait() a copy / accumulation of the unfinished blocks
+        watch = []
+        seen = set()
+        for t in (means3D, sh) + tuple(inputs) + self._params:
+            if isinstance(t, torch.Tensor) and t.is_leaf and t.requires_grad and id(t) not in seen:
+                seen.add(id(t))
+                gr = t.grad
+                watch.append((t, gr, None if gr is None else gr._version))
+        self.entries.append(dict(rows=rows, B=B, means3D=means3D.detach(), sh=sh.detach(), degree=int(degree),
+                                 arena=arena, P=P, M=M, watch=watch))
 
     def start(self):
         if not self.entries:
@@ -138,9 +165,11 @@ class ShExchange:
         return _ShExchangeHandle([self._start_one(e) for e in entries])
 
     def _start_one(self, e):
-        P, M = int(e["means3D"].size(0)), int(e["sh"].size(1))
+        P, M = e["P"], e["M"]
         lay = arena_layout(P, M)
         arena, rows = e["arena"], e["rows"]
+        dsh = arena.narrow(0, lay["dsh"][0], 3 * M * P).view(P, M, 3)
+        dmeans3D = arena.narrow(0, lay["dmeans3D"][0], 3 * P).view(P, 3)
         world = dist.get_world_size(self.group)
         xyz = arena.narrow(0, lay["dmeans3D"][0], 3 * P)
         o_rest = lay["dopacity"][0]
@@ -158,19 +187,19 @@ class ShExchange:
         if not cuda:
             for w in works:
                 w.wait()
-            fn(rows_all, V, e["means3D"], e["sh"], e["degree"], e["dsh"], e["dmeans3D"])
-            return (None, keep)
+            fn(rows_all, V, e["means3D"], e["sh"], e["degree"], dsh, dmeans3D)
+            return (None, keep, e)
         side = _side_stream(rows.device)
         side.wait_stream(torch.cuda.current_stream(rows.device))
         with torch.cuda.stream(side):
             for w in works:
                 w.wait()  # stream-side wait on the collective
-            fn(rows_all, V, e["means3D"], e["sh"], e["degree"], e["dsh"], e["dmeans3D"])
+            fn(rows_all, V, e["means3D"], e["sh"], e["degree"], dsh, dmeans3D)
             ev = torch.cuda.Event()
             ev.record(side)
         for t in keep:
             t.record_stream(side)
-        return (ev, keep)
+        return (ev, keep, e)
 
 
 _SIDE = {}
@@ -187,7 +216,28 @@ class _ShExchangeHandle:
         self.parts = parts
 
     def wait(self):
-        for ev, _ in self.parts:
+        for ev, _, e in self.parts:
             if ev is not None:
                 torch.cuda.current_stream().wait_event(ev)
+            _check_leaf_grads(e)
         self.parts = []
+
+
+def _aliases(t, arena):
+    """t lies inside the gradient arena's memory (it is one of the backward's views)."""
+    a0 = arena.data_ptr()
+    return a0 <= t.data_ptr() < a0 + arena.numel() * arena.element_size()
+
+
+def _check_leaf_grads(e):
+    for leaf, before, version in e["watch"]:
+        g = leaf.grad
+        if g is None or _aliases(g, e["arena"]):
+            continue  # untouched (torch.autograd.grad) or handed over without a copy
+        if g is before and g._version == version:
+            continue  # a .grad from before this backward, not written by it
+        raise RuntimeError(
+            "ShExchange: autograd copied or accumulated the deferred SH-path gradients into a leaf's .grad "
+            "before the exchange completed them (the leaf had a .grad already, or the gradient was reshaped "
+            "on its way to the leaf).  Use torch.autograd.grad, zero_grad(set_to_none=True) before "
+            "loss.backward(), or gsr_train's arena parameters.")

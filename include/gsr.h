@@ -27,6 +27,11 @@
  *     auxiliary.h:166-173).
  *   - No global mutable device state: concurrent calls on distinct buffers and
  *     streams are safe (one process per GPU under torchrun).
+ *   - Supersets of the reference's behaviour (no result the reference computes
+ *     changes): settings->prefiltered = 1 never traps -- a Gaussian outside the
+ *     frustum is culled as with prefiltered = 0 (the reference traps the whole
+ *     kernel on one, auxiliary.h:156-160; its trainer always passes False);
+ *     gradients are deterministic (no float atomics).
  */
 #ifndef GSR_H_
 #define GSR_H_
@@ -219,8 +224,9 @@ GSR_API int gsr_mark_visible(int P, const float* means3D, const float* viewmatri
  * types: "tiles_touched" u32[P], "rec" f32[P,16] ({x,y,conic.xyz,opacity,depth,
  * seg0,r,g,b,seg1,0...}), "clamped" u8[P], "order" u32[P] (depth order),
  * "goff" u32[P], "point_list" u32[I], "slot_vals" u32[I], "ranges" u32[T,2],
- * "n_contrib_tiles" u32[T,256] (tile-major, entry k*64+l = pixel
- * (16*tx + (l&15), 16*ty + (l>>4) + 4k)).  Returns the byte count copied, or -1. */
+ * "n_contrib_tiles" u32[T,256] (tile-major, in the forward's 8x8-quadrant layout:
+ * entry k*64+l of tile (tx, ty) is pixel (16*tx + 8*(k&1) + (l&7), 16*ty + 8*(k>>1) + (l>>3)),
+ * k = 0..3 the quadrant, l = 0..63 the lane).  Returns the byte count copied, or -1. */
 GSR_API long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered, int binning_capacity,
                                  void* geom, void* binning, void* img, void* dst, void* stream);
 

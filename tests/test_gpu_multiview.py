@@ -141,7 +141,7 @@ class _Sink:
         from diff_gaussian_rasterization import _C
         return torch.full((B * _C.sh_rows_floats(P),), float("nan"), dtype=torch.float32, device=device)
 
-    def record(self, rows, B, means3D, sh, degree, dsh, dmeans3D):
+    def record(self, rows, B, means3D, sh, degree, dsh, dmeans3D, inputs=()):
         self.entries.append((rows, B, means3D, sh, degree, dsh, dmeans3D))
 
 

@@ -4,15 +4,17 @@ Tolerances (north_star: bit-exact tile/key indexing, 1e-5 fp32 on images and gra
   * integer outputs -- radii, tiles_touched, num_rendered, point_list (the sorted
     (tile, depth, gaussian) order), ranges and per-pixel n_contrib -- bit-exact;
   * images (color, depth, alpha, segment): |gsr - oracle| <= 1e-5 * max(1, |oracle|)
-    for every pixel;
-  * gradients: |gsr - oracle| <= 1e-5 * max(1, max|oracle|) for every element
-    (normwise per tensor; the oracle sums gradient terms exactly, the reference's
-    atomicAdd order is arbitrary).
+    for every pixel (image values are O(1));
+  * gradients: |gsr - oracle| <= 1e-5 * max|oracle| for every element, per tensor
+    (scale-free: no floor, so the bound is 1e-5 of the largest element whatever the
+    scale of the upstream gradients; the oracle sums gradient terms exactly, the
+    reference's atomicAdd order is arbitrary).
 The kernels and the oracle share one IEEE-only exp (gsr_expf), so the knife-edge
 blend decisions (alpha >= 1/255, T(1-alpha) >= 1e-4, forward.cu:352-359) agree
-exactly; the *_OUTLIER_* budgets below are therefore 0.  (With the C library's
-expf in the oracle instead, up to ~2e-3 of the gradient elements move by up to
-1.4e-4 at the metric config: tools/noise_diag.py)
+exactly; the *_OUTLIER_* budgets below are therefore 0.  Against an oracle that
+blends with the C library's expf instead (an exp independent of gsr, standing in
+for the reference's CUDA expf), knife-edge outliers appear; their budget is stated
+and tested in test_gpu_exp_budget.py.
 """
 import math
 
@@ -57,7 +59,10 @@ def assert_grad_parity(g, r):
         b = ref.astype(np.float64)
         if k == "dmeans2D":
             a, b = a[:, :2], b[:, :2]
-        scale = max(1.0, float(np.abs(b).max()) if b.size else 1.0)
+        scale = float(np.abs(b).max()) if b.size else 0.0
+        if scale == 0.0:  # an all-zero reference gradient must be matched exactly
+            assert not np.any(a), f"{k}: reference is all zero, gsr max |g| = {np.abs(a).max():.3e}"
+            continue
         err = np.abs(a - b) / scale
         frac = float((err > GRAD_TOL).mean()) if err.size else 0.0
         assert frac <= GRAD_OUTLIER_FRAC, f"{k}: {frac:.2e} of elements above {GRAD_TOL} (max {err.max():.3e})"

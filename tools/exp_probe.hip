@@ -11,7 +11,8 @@
 #include <cstring>
 #include <cstdlib>
 
-__global__ void k_probe(uint32_t b0, uint32_t n, unsigned long long* hist, uint32_t* worst) {
+__global__ void k_probe(uint32_t b0, uint32_t n, unsigned long long* hist, uint32_t* worst, uint32_t* list,
+                        uint32_t cap) {
     uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t stride = gridDim.x * blockDim.x;
     unsigned long long h[5] = {0, 0, 0, 0, 0};
@@ -24,10 +25,10 @@ __global__ void k_probe(uint32_t b0, uint32_t n, unsigned long long* hist, uint3
         const int ad = d < 0 ? -d : d;
         h[ad > 3 ? 4 : ad]++;
         if (ad > 0) atomicMax(worst, (uint32_t)ad);
-        if (ad > 0 && ad < 1000) {
-            // keep the first few mismatching inputs for inspection
+        if (ad > 0) {
+            // keep every mismatching input (up to cap) for the oracle's exception table
             unsigned int slot = atomicAdd(&worst[1], 1u);
-            if (slot < 16) worst[2 + slot] = bits;
+            if (slot < cap) { list[2 * slot] = bits; list[2 * slot + 1] = __float_as_uint(hw); }
         }
     }
     for (int k = 0; k < 5; ++k)
@@ -46,7 +47,10 @@ int main(int argc, char** argv) {
     hipMalloc(&worst, 18 * sizeof(uint32_t));
     hipMemset(hist, 0, 5 * sizeof(unsigned long long));
     hipMemset(worst, 0, 18 * sizeof(uint32_t));
-    hipLaunchKernelGGL(k_probe, dim3(8192), dim3(256), 0, 0, b0, n, hist, worst);
+    const uint32_t cap = 1u << 24;
+    uint32_t* list;
+    hipMalloc(&list, 2ull * cap * sizeof(uint32_t));
+    hipLaunchKernelGGL(k_probe, dim3(8192), dim3(256), 0, 0, b0, n, hist, worst, list, cap);
     // positive side too (y in [0, 1]), small
     unsigned long long h[5];
     uint32_t w[18];
@@ -55,10 +59,20 @@ int main(int argc, char** argv) {
     printf("range [%g, -0]: %u inputs\n", lo, n);
     printf("ulp diff 0: %llu  1: %llu  2: %llu  3: %llu  >3: %llu  worst %u  mismatches %u\n", h[0], h[1], h[2],
            h[3], h[4], w[0], w[1]);
-    for (int k = 0; k < 16 && k < (int)w[1]; ++k) {
-        float y;
-        memcpy(&y, &w[2 + k], 4);
-        printf("  mismatch y=%.9g (0x%08x)\n", y, w[2 + k]);
+    const uint32_t m = w[1] < cap ? w[1] : cap;
+    uint32_t* hl = (uint32_t*)malloc(2ull * m * sizeof(uint32_t) + 8);
+    hipMemcpy(hl, list, 2ull * m * sizeof(uint32_t), hipMemcpyDeviceToHost);
+    for (uint32_t k = 0; k < 16 && k < m; ++k) {
+        float y, e;
+        memcpy(&y, &hl[2 * k], 4);
+        memcpy(&e, &hl[2 * k + 1], 4);
+        printf("  mismatch y=%.9g (0x%08x) hw=%.9g cr=%.9g\n", y, hl[2 * k], e, (float)exp2((double)y));
+    }
+    if (argc > 2) {  // dump (input bits, hw bits) pairs
+        FILE* f = fopen(argv[2], "wb");
+        fwrite(hl, 8, m, f);
+        fclose(f);
+        printf("wrote %u pairs to %s\n", m, argv[2]);
     }
     return 0;
 }
