@@ -262,7 +262,7 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
         const bool lb = sort_uses_lookback(P);
         launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
                           at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect),
-                          packed ? at<uint32_t>(g, L.rect32) : nullptr,
+                          packed ? at<uint32_t>(g, L.rect32) : nullptr, at<float>(g, L.shjac),
                           g + L.ws, lb ? sort_lb_zero_bytes(P, depth_sort_passes(), sort_lb_items()) : 0,
                           g + L.ws_scan, scan_ws_bytes(P), st);
     }
@@ -358,7 +358,7 @@ int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* b
             StageScope sc(GSR_STAGE_TILE_SORT, st);
             // the last pass also produces the tile ranges (identifyTileRanges,
             // rasterizer_impl.cu:113-138) and clears the backward's written-slot mask
-            const SortFinal fin{ranges, at<uint4>(b, BL.written), cdiv(I, 128)};
+            const SortFinal fin{ranges, at<uint4>(b, BL.written), cdiv(I, 16)};
             launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout, at<uint32_t>(b, BL.slot_vals),
                               I, bits, b + BL.ws, /*ws_zeroed=*/false, st,
                               at<uint32_t>(b, BL.slot_gid), at<uint32_t>(b, BL.gid_alt),
@@ -432,13 +432,13 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
     const GeomLayout GL = geom_layout(P);
     char* g = aligned_base(geom);
     float* contrib = nullptr;
-    uint32_t* written = nullptr;
+    uint8_t* written = nullptr;
     if (I > 0) {
         if (!binning || !scratch) return fail("[gsr] binning/scratch buffer is NULL");
         const BinLayout BL = bin_layout(bin_cap(s, I));
         char* b = aligned_base(binning);
         contrib = reinterpret_cast<float*>(aligned_base(scratch));
-        written = at<uint32_t>(b, BL.written);  // cleared by the forward's tile sort
+        written = at<uint8_t>(b, BL.written);  // cleared by the forward's tile sort
         {
             StageScope sc(GSR_STAGE_RENDER_BWD, st);
             launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order), at<uint2>(im, IL.ranges),
@@ -451,7 +451,8 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
     {
         StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);
         launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
-                                 at<uint8_t>(g, GL.clamped), contrib, written, at<float4>(g, GL.rec), *grads, st);
+                                 at<uint8_t>(g, GL.clamped), contrib, written, at<float4>(g, GL.rec),
+                                 at<float>(g, GL.shjac), *grads, st);
     }
     GSR_STAGE("gaussian backward");
     return 0;
@@ -501,13 +502,13 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
         const GeomLayout GL = geom_layout(P);
         char* g = aligned_base(V.geom);
         float* contrib = nullptr;
-        uint32_t* written = nullptr;
+        uint8_t* written = nullptr;
         if (I > 0) {
             if (!V.binning || !V.scratch) return fail("[gsr] multiview: binning/scratch buffer is NULL");
             const BinLayout BL = bin_layout(bin_cap(V.s, I));
             char* b = aligned_base(V.binning);
             contrib = reinterpret_cast<float*>(aligned_base(V.scratch));
-            written = at<uint32_t>(b, BL.written);
+            written = at<uint8_t>(b, BL.written);
             {
                 StageScope sc(GSR_STAGE_RENDER_BWD, st);
                 launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order),

@@ -261,34 +261,34 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restric
 // identity on them and is skipped (k_radix_scatter copies the tile through).
 // Keys per thread of k_radix_hist: fewer, fuller blocks mean fewer global atomics at the
 // end (one per nonzero (pass, digit) per block).
-#ifndef GSR_HIST_ITEMS
-#define GSR_HIST_ITEMS 16
-#endif
-constexpr int HIST_ITEMS = GSR_HIST_ITEMS;
-__global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __restrict__ keys, size_t n,
+// 16 waves x 4 keys per thread per block (a 4-wave block with 16 keys per thread left
+// under one wave per SIMD at 1M keys: latency-bound, 16 us).
+constexpr int HIST_THREADS = 1024, HIST_ITEMS = 4;
+__global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __restrict__ keys, size_t n,
                                                              int passes, int per_pass, int key_bits,
                                                              uint32_t* __restrict__ hist, uint32_t* span,
                                                              int skip_sentinel, const uint32_t* n_dev) {
     if (n_dev) n = min(n, (size_t)*n_dev);
     __shared__ uint32_t cnt[4][RADIX];
     __shared__ uint32_t s_span[8];
+    if (threadIdx.x < RADIX)
 #pragma unroll
-    for (int p = 0; p < 4; ++p) cnt[p][threadIdx.x] = 0;
+        for (int p = 0; p < 4; ++p) cnt[p][threadIdx.x] = 0;
     if (threadIdx.x < 8) s_span[threadIdx.x] = 0;
     __syncthreads();
     uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};  // max(256 - d), max(d + 1)
-    // HIST_ITEMS keys per thread, all loads issued before any use (a strided loop with
-    // one dependent load per iteration is latency-bound).
-    const size_t base = (size_t)blockIdx.x * SORT_THREADS * HIST_ITEMS + threadIdx.x;
+    // all loads issued before any use (a strided loop with one dependent load per
+    // iteration is latency-bound)
+    const size_t base = (size_t)blockIdx.x * HIST_THREADS * HIST_ITEMS + threadIdx.x;
     uint32_t kk[HIST_ITEMS];
 #pragma unroll
     for (int i = 0; i < HIST_ITEMS; ++i) {
-        const size_t idx = base + (size_t)i * SORT_THREADS;
+        const size_t idx = base + (size_t)i * HIST_THREADS;
         kk[i] = idx < n ? keys[idx] : 0u;
     }
 #pragma unroll
     for (int i = 0; i < HIST_ITEMS; ++i) {
-        const size_t idx = base + (size_t)i * SORT_THREADS;
+        const size_t idx = base + (size_t)i * HIST_THREADS;
         const bool valid = idx < n;
         const uint32_t k = kk[i];
         const uint64_t vmask = __ballot(valid);
@@ -326,8 +326,9 @@ __global__ void __launch_bounds__(SORT_THREADS) k_radix_hist(const uint32_t* __r
         }
     }
     __syncthreads();
-    for (int p = 0; p < passes; ++p)
-        if (cnt[p][threadIdx.x]) atomicAdd(&hist[p * RADIX + threadIdx.x], cnt[p][threadIdx.x]);
+    if (threadIdx.x < RADIX)
+        for (int p = 0; p < passes; ++p)
+            if (cnt[p][threadIdx.x]) atomicAdd(&hist[p * RADIX + threadIdx.x], cnt[p][threadIdx.x]);
     if (threadIdx.x < 2 * passes && s_span[threadIdx.x]) atomicMax(&span[threadIdx.x], s_span[threadIdx.x]);
 }
 
@@ -590,34 +591,58 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
 // tiles first turns it into a longest-processing-time-first scheduler (the
 // natural row-major order leaves the dense centre tiles for the end).  Order
 // within a bucket is arbitrary: it changes timing only, never a result.
-__global__ void __launch_bounds__(1024) k_tile_order(uint2* __restrict__ ranges, int T,
-                                                     uint32_t* __restrict__ order) {
-    __shared__ uint32_t hist[33], off[33];
-    const int tid = threadIdx.x;
-    if (tid < 33) hist[tid] = 0;
+__device__ __forceinline__ uint32_t len_bucket(uint2 r) {
+    const uint32_t len = r.y - r.x;
+    return len ? 32 - __clz(len) : 0;
+}
+
+// Counters are private to each wave (LDS [wave][bucket]): a lane's atomic contends only
+// with its own wave's lanes inside one instruction.  Shared counters serialised across
+// the whole block when most tiles share a bucket (at the 6M-Gaussian config every tile
+// length has the same bit length: 0.1 ms).
+constexpr int ORDER_THREADS = 1024, ORDER_WAVES = ORDER_THREADS / 64;
+__global__ void __launch_bounds__(ORDER_THREADS) k_tile_order(uint2* __restrict__ ranges, int T,
+                                                              uint32_t* __restrict__ order) {
+    __shared__ uint32_t wcnt[ORDER_WAVES][33];
+    const int tid = threadIdx.x, wave = tid >> 6;
+    for (int i = tid; i < ORDER_WAVES * 33; i += ORDER_THREADS) (&wcnt[0][0])[i] = 0;
     __syncthreads();
-    for (int t = tid; t < T; t += blockDim.x) {
+#pragma unroll 4
+    for (int t = tid; t < T; t += ORDER_THREADS) {
         uint2 r = ranges[t];
         if (r.x == ~0u) {  // no instance (the tile sort's atomicMin never touched it): {0, 0}
             r = make_uint2(0u, 0u);
             ranges[t] = r;
         }
-        const uint32_t len = r.y - r.x;
-        atomicAdd(&hist[len ? 32 - __clz(len) : 0], 1u);
+        atomicAdd(&wcnt[wave][len_bucket(r)], 1u);
     }
     __syncthreads();
-    if (tid == 0) {
+    __shared__ uint32_t btot[33], boff[33];
+    if (tid < 33) {  // per bucket: wave bases inside the bucket, and its total
         uint32_t run = 0;
-        for (int b = 32; b >= 0; --b) {
-            off[b] = run;
-            run += hist[b];
+        for (int w = 0; w < ORDER_WAVES; ++w) {
+            const uint32_t c = wcnt[w][tid];
+            wcnt[w][tid] = run;
+            run += c;
         }
+        btot[tid] = run;
     }
     __syncthreads();
-    for (int t = tid; t < T; t += blockDim.x) {
-        const uint2 r = ranges[t];
-        const uint32_t len = r.y - r.x;
-        order[atomicAdd(&off[len ? 32 - __clz(len) : 0], 1u)] = (uint32_t)t;
+    if (tid < 64) {  // heavy buckets first: exclusive scan over buckets 32, 31, ..., 0
+        const uint32_t v = tid < 33 ? btot[32 - tid] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if (tid >= o) x += y;
+        }
+        if (tid < 33) boff[32 - tid] = x - v;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int t = tid; t < T; t += ORDER_THREADS) {
+        const uint32_t b = len_bucket(ranges[t]);
+        order[boff[b] + atomicAdd(&wcnt[wave][b], 1u)] = (uint32_t)t;
     }
 }
 
@@ -697,7 +722,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     if (lb) {
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);
-        hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)cdiv(n, (size_t)SORT_THREADS * HIST_ITEMS)), dim3(SORT_THREADS), 0, st, keys_in,
+        hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)cdiv(n, (size_t)HIST_THREADS * HIST_ITEMS)), dim3(HIST_THREADS), 0, st, keys_in,
                            n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel, n_dev);
     }
     const uint32_t* kin = keys_in;

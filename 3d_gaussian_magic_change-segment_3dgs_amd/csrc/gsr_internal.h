@@ -92,7 +92,7 @@ inline SortWs sort_ws(size_t n, void* p) {
 // ---- geometry buffer (reference GeometryState, rasterizer_impl.cu:155-171) ----
 struct GeomLayout {
     size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, goff, ws,
-        ws_scan, rect32, rect32_alt, rect32_sorted, bytes;
+        ws_scan, rect32, rect32_alt, rect32_sorted, shjac, bytes;
 };
 inline GeomLayout geom_layout(size_t P) {
     GeomLayout L{};
@@ -116,6 +116,9 @@ inline GeomLayout geom_layout(size_t P) {
     L.rect32 = take(P * 4);
     L.rect32_alt = take(P * 4);
     L.rect32_sorted = take(P * 4);
+    // d(rgb)/d(dir) of the SH colour, 9 x 64 floats per 64 Gaussians (preprocess writes
+    // it, the backward reads it instead of the 192-B SH rows; preprocess.hip sh_dir_jacobian)
+    L.shjac = take(cdiv(P, 64) * 64 * 9 * 4);
     L.bytes = o + ALIGN;
     return L;
 }
@@ -135,7 +138,7 @@ inline BinLayout bin_layout(size_t I) {
     L.slot_gid = take(I * 4);
     L.gid_alt = take(I * 4);
     L.point_list = take(I * 4);
-    L.written = take(cdiv(I, 128) * 16);  // backward: 1 bit per instance slot (zeroed by the tile sort's last pass)
+    L.written = take(cdiv(I, 16) * 16);  // backward: 1 byte per instance slot (zeroed by the tile sort's last pass)
     L.ws = take(sort_ws_bytes(I, MAX_SORT_PASSES));
     L.bytes = o + ALIGN;
     return L;
@@ -172,8 +175,8 @@ inline char* aligned_base(void* p) {
 // preprocess.hip
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec,
                        int* radii, uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped,
-                       ushort4* rect, uint32_t* rect32, void* zero_a, size_t zero_a_bytes, void* zero_b,
-                       size_t zero_b_bytes, hipStream_t st);
+                       ushort4* rect, uint32_t* rect32, float* shjac, void* zero_a, size_t zero_a_bytes,
+                       void* zero_b, size_t zero_b_bytes, hipStream_t st);
 // the packed rect (GeomLayout::rect32) fits grids of up to 255 x 255 tiles (4080 px)
 inline bool rect_packable(int gx, int gy) { return gx <= 255 && gy <= 255; }
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
@@ -184,7 +187,7 @@ struct MvView {
     const uint32_t* goff;
     const uint8_t* clamped;
     const float* contrib;
-    const uint32_t* written;
+    const uint8_t* written;
     const float4* rec;
     const float* view;
     const float* proj;
@@ -208,8 +211,8 @@ void launch_sh_backward(int P, int D, int M, const float* shs, const float* mean
                         float* dsh, float* dmeans3D, hipStream_t st);
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const uint32_t* written, const float4* rec,
-                              const gsr_grads& g, hipStream_t st);
+                              const float* contrib, const uint8_t* written, const float4* rec,
+                              const float* shjac, const gsr_grads& g, hipStream_t st);
 // binning.hip
 // Optional last-pass outputs of a sort: ranges[key] = [first, last + 1) of each key's run in
 // the sorted order (atomicMin/atomicMax per run and tile; empty keys keep {~0u, 0}, which
@@ -249,7 +252,7 @@ void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order,
                             const uint32_t* point_list,
                             const uint32_t* slot_vals, const float4* rec, const float* bg, const float* alpha,
                             const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_dsegment,
-                            const float* dL_ddepth, const float* dL_dalpha, float* contrib, uint32_t* written,
+                            const float* dL_ddepth, const float* dL_dalpha, float* contrib, uint8_t* written,
                             hipStream_t st);
 
 uint32_t higher_msb(uint32_t n);

@@ -210,6 +210,84 @@ __device__ __forceinline__ f3 color_from_sh(int deg, f3 dir, const SF& S, uint8_
     return {fmaxf(result.x, 0.0f), fmaxf(result.y, 0.0f), fmaxf(result.z, 0.0f)};
 }
 
+// The direction Jacobian of the SH colour, d(rgb)/d(dir) as three f3 over the colour
+// channels (dx, dy, dz: the dRGBdx / dRGBdy / dRGBdz of backward.cu:54-107), written in
+// the reference's evaluation order.  The forward evaluates it while the SH row is at
+// hand (LDS) and stores it (GeomLayout::shjac, wave-blocked SoA); the backward then needs
+// no SH coefficients at all: dL/ddir = (dx . dRGB, dy . dRGB, dz . dRGB)
+// (backward.cu:109-111) from 36 B per Gaussian instead of a 192-B SH row.  The same
+// expressions under the same contraction setting: bit-identical to evaluating them in
+// the backward, as the reference and the oracle do.
+template <typename SF>
+__device__ __forceinline__ void sh_dir_jacobian(int deg, f3 dir, const SF& S, f3& dx, f3& dy, f3& dz) {
+    dx = {0, 0, 0};
+    dy = {0, 0, 0};
+    dz = {0, 0, 0};
+    const float x = dir.x, y = dir.y, z = dir.z;
+    if (deg > 0) {
+        dx = -C_SH1 * S(3);
+        dy = -C_SH1 * S(1);
+        dz = C_SH1 * S(2);
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            dx = dx + (C_SH2[0] * y * S(4) + C_SH2[2] * 2.f * -x * S(6) + C_SH2[3] * z * S(7) +
+                       C_SH2[4] * 2.f * x * S(8));
+            dy = dy + (C_SH2[0] * x * S(4) + C_SH2[1] * z * S(5) + C_SH2[2] * 2.f * -y * S(6) +
+                       C_SH2[4] * 2.f * -y * S(8));
+            dz = dz + (C_SH2[1] * y * S(5) + C_SH2[2] * 2.f * 2.f * z * S(6) + C_SH2[3] * x * S(7));
+            if (deg > 2) {
+                dx = dx + (C_SH3[0] * S(9) * 3.f * 2.f * xy + C_SH3[1] * S(10) * yz +
+                           C_SH3[2] * S(11) * -2.f * xy + C_SH3[3] * S(12) * -3.f * 2.f * xz +
+                           C_SH3[4] * S(13) * (-3.f * xx + 4.f * zz - yy) + C_SH3[5] * S(14) * 2.f * xz +
+                           C_SH3[6] * S(15) * 3.f * (xx - yy));
+                dy = dy + (C_SH3[0] * S(9) * 3.f * (xx - yy) + C_SH3[1] * S(10) * xz +
+                           C_SH3[2] * S(11) * (-3.f * yy + 4.f * zz - xx) + C_SH3[3] * S(12) * -3.f * 2.f * yz +
+                           C_SH3[4] * S(13) * -2.f * xy + C_SH3[5] * S(14) * -2.f * yz +
+                           C_SH3[6] * S(15) * -3.f * 2.f * xy);
+                dz = dz + (C_SH3[1] * S(10) * xy + C_SH3[2] * S(11) * 4.f * 2.f * yz +
+                           C_SH3[3] * S(12) * 3.f * (2.f * zz - xx - yy) + C_SH3[4] * S(13) * 4.f * 2.f * xz +
+                           C_SH3[5] * S(14) * (xx - yy));
+            }
+        }
+    }
+}
+
+// Jacobian storage: per 64 consecutive Gaussians a block of 9 rows x 64 floats (component
+// k of Gaussian i at block(i) + 64 k + (i & 63)): every access is a coalesced 256-B row
+// and the 9 addresses of a thread are one base plus immediate offsets.
+__device__ __forceinline__ float* jac_row(float* J, int idx) { return J + (size_t)(idx & ~63) * 9 + (idx & 63); }
+__device__ __forceinline__ const float* jac_row(const float* J, int idx) {
+    return J + (size_t)(idx & ~63) * 9 + (idx & 63);
+}
+
+// SH basis values bas[i] = dRGB/dsh[i] (backward.cu:46-107); entries >= (deg+1)^2 are 0.
+__device__ __forceinline__ void sh_basis(int deg, f3 dir, float bas[16]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) bas[i] = 0.f;
+    const float x = dir.x, y = dir.y, z = dir.z;
+    bas[0] = C_SH0;
+    if (deg > 0) {
+        bas[1] = -C_SH1 * y; bas[2] = C_SH1 * z; bas[3] = -C_SH1 * x;
+        if (deg > 1) {
+            const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
+            bas[4] = C_SH2[0] * xy;
+            bas[5] = C_SH2[1] * yz;
+            bas[6] = C_SH2[2] * (2.f * zz - xx - yy);
+            bas[7] = C_SH2[3] * xz;
+            bas[8] = C_SH2[4] * (xx - yy);
+            if (deg > 2) {
+                bas[9] = C_SH3[0] * y * (3.f * xx - yy);
+                bas[10] = C_SH3[1] * xy * z;
+                bas[11] = C_SH3[2] * y * (4.f * zz - xx - yy);
+                bas[12] = C_SH3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
+                bas[13] = C_SH3[4] * x * (4.f * zz - xx - yy);
+                bas[14] = C_SH3[5] * z * (xx - yy);
+                bas[15] = C_SH3[6] * x * (xx - 3.f * yy);
+            }
+        }
+    }
+}
+
 struct Cam {
     float view[16], proj[16];
     f3 campos;
@@ -230,7 +308,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
                                                     uint32_t* __restrict__ tiles_touched,
                                                     uint32_t* __restrict__ depth_keys,
                                                     uint8_t* __restrict__ clamped, ushort4* __restrict__ rect,
-                                                    uint32_t* __restrict__ rect32,
+                                                    uint32_t* __restrict__ rect32, float* __restrict__ shjac,
                                                     void* zero_a, size_t zero_a16, void* zero_b, size_t zero_b16) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     // clear the depth sort's and the scan's look-back counters (saves two memset launches)
@@ -298,6 +376,15 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
 
     f3 rgb = {0.f, 0.f, 0.f};
     uint8_t cbits = 0;
+    // the SH direction Jacobian goes straight out (ok is final here): no live range
+    // across the LDS passes.  Coalesced 256-B rows (jac_row).
+    auto store_jac = [&](f3 jx, f3 jy, f3 jz) {
+        float* J = jac_row(shjac, idx);
+        J[0] = jx.x; J[64] = jx.y; J[128] = jx.z;
+        J[192] = jy.x; J[256] = jy.y; J[320] = jy.z;
+        J[384] = jz.x; J[448] = jz.y; J[512] = jz.z;
+    };
+    const bool want_jac = shjac && s.D > 0;
     if (in.colors_precomp == nullptr) {
         f3 dir = p_orig - cam.campos;
         dir = dir / sqrtf(dot3(dir, dir));
@@ -327,8 +414,13 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
                 __syncthreads();
                 if ((lane >> 5) == h && ok) {
                     const float* S = shrow[wave][lane & 31];
-                    rgb = color_from_sh(s.D, dir, [&](int i) { return f3{S[3 * i], S[3 * i + 1], S[3 * i + 2]}; },
-                                        cbits);
+                    auto Sf = [&](int i) { return f3{S[3 * i], S[3 * i + 1], S[3 * i + 2]}; };
+                    rgb = color_from_sh(s.D, dir, Sf, cbits);
+                    if (want_jac) {
+                        f3 jx, jy, jz;
+                        sh_dir_jacobian(s.D, dir, Sf, jx, jy, jz);
+                        store_jac(jx, jy, jz);
+                    }
                 }
                 __syncthreads();
             }
@@ -336,7 +428,13 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
             // per-coefficient loads: here they overlap the projection math better than a
             // row of float4 loads issued up front (measured: 0.091 vs 0.100 ms at 1M)
             const float* sh = in.shs + (size_t)idx * s.M * 3;
-            rgb = color_from_sh(s.D, dir, [&](int i) { return ld3(sh + 3 * i); }, cbits);
+            auto Sf = [&](int i) { return ld3(sh + 3 * i); };
+            rgb = color_from_sh(s.D, dir, Sf, cbits);
+            if (want_jac) {
+                f3 jx, jy, jz;
+                sh_dir_jacobian(s.D, dir, Sf, jx, jy, jz);
+                store_jac(jx, jy, jz);
+            }
         }
     } else if (ok) {
         rgb = ld3(in.colors_precomp + 3 * (size_t)idx);
@@ -388,23 +486,42 @@ __global__ void k_mark_visible(int P, const float* __restrict__ means3D, const f
 // a sequential fp32 rounding error per tile, which the cov2D backward amplifies by
 // 1/det(cov2D)^2 for elongated Gaussians (C5: dscales off by 1.3e-5 of the tensor max
 // in fp32).  The kernel is HBM-bound; the fp64 adds cost no time.
-__device__ __forceinline__ void sum_records(const float* __restrict__ contrib, const uint32_t* __restrict__ written,
+__device__ __forceinline__ void sum_records(const float* __restrict__ contrib, const uint8_t* __restrict__ written,
                                             uint32_t lo, uint32_t hi, float q[12]) {
     double d[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) d[j] = 0.0;
-    for (uint32_t w = lo >> 5; w <= (hi - 1) >> 5; ++w) {
-        uint32_t bits = written[w];
-        if (w == lo >> 5) bits &= ~0u << (lo & 31);
-        if (w == (hi - 1) >> 5 && ((hi & 31) != 0)) bits &= ~(~0u << (hi & 31));
+    // Written flags (one byte per slot, 0 or 1) are read 8 at a time and folded into an
+    // 8-bit mask (byte i -> bit i); then four records per round, their loads issued
+    // together (clamped slot indices: a record-at-a-time loop leaves one load in flight
+    // per lane).  Sums stay in slot order.
+    const uint64_t* w8 = reinterpret_cast<const uint64_t*>(written);
+    for (uint32_t w = lo >> 3; w <= (hi - 1) >> 3; ++w) {
+        uint32_t bits = (uint32_t)(((w8[w] & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+        if (w == lo >> 3) bits &= 0xFFu << (lo & 7);
+        if (w == (hi - 1) >> 3 && ((hi & 7) != 0)) bits &= ~(0xFFu << (hi & 7));
         while (bits) {
-            const uint32_t u = (w << 5) + (uint32_t)__builtin_ctz(bits);
-            bits &= bits - 1;
-            const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)u * 12);
-            const float4 a = src[0], b = src[1], c = src[2];
-            d[0] += a.x; d[1] += a.y; d[2] += a.z; d[3] += a.w;
-            d[4] += b.x; d[5] += b.y; d[6] += b.z; d[7] += b.w;
-            d[8] += c.x; d[9] += c.y; d[10] += c.z; d[11] += c.w;
+            uint32_t u[4];
+            bool v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                v[k] = bits != 0;
+                u[k] = v[k] ? (w << 3) + (uint32_t)__builtin_ctz(bits) : u[0];
+                bits &= bits - 1;
+            }
+            float4 r[4][3];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)u[k] * 12);
+                r[k][0] = src[0]; r[k][1] = src[1]; r[k][2] = src[2];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (!v[k]) continue;
+                d[0] += r[k][0].x; d[1] += r[k][0].y; d[2] += r[k][0].z; d[3] += r[k][0].w;
+                d[4] += r[k][1].x; d[5] += r[k][1].y; d[6] += r[k][1].z; d[7] += r[k][1].w;
+                d[8] += r[k][2].x; d[9] += r[k][2].y; d[10] += r[k][2].z; d[11] += r[k][2].w;
+            }
         }
     }
 #pragma unroll
@@ -430,8 +547,9 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
                                                            const uint32_t* __restrict__ goff,
                                                            const uint8_t* __restrict__ clamped,
                                                            const float* __restrict__ contrib,
-                                                           const uint32_t* __restrict__ written,
-                                                           const float4* __restrict__ rec, gsr_grads g) {
+                                                           const uint8_t* __restrict__ written,
+                                                           const float4* __restrict__ rec,
+                                                           const float* __restrict__ shjac, gsr_grads g) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const int M = s.M;
     const size_t i3 = 3 * (size_t)idx;
@@ -572,10 +690,9 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         dmean = dmean + dm2;
 
         if (in.shs) {
-            // computeColorFromSH backward (backward.cu:20-139)
+            // computeColorFromSH backward (backward.cu:20-139), from the direction Jacobian
+            // the forward stored (sh_dir_jacobian): no SH coefficient is read here
             const int deg = s.D;
-            ShRow S;
-            S.load(in.shs + (size_t)idx * M * 3, M, (deg + 1) * (deg + 1));
             const f3 dir_orig = m - cam.campos;
             const f3 dir = dir_orig / sqrtf(dot3(dir_orig, dir_orig));
             const uint8_t cb = clamped[idx];
@@ -584,48 +701,14 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
             dRGB.y *= (cb & 2) ? 0 : 1;
             dRGB.z *= (cb & 4) ? 0 : 1;
             f3 dx = {0, 0, 0}, dy = {0, 0, 0}, dz = {0, 0, 0};
-            const float x = dir.x, y = dir.y, z = dir.z;
-            // dL/dsh[i] = basis_i * dRGB (backward.cu:46-110); coefficients >= (D+1)^2 get 0
-            bas[0] = C_SH0;
             if (deg > 0) {
-                bas[1] = -C_SH1 * y; bas[2] = C_SH1 * z; bas[3] = -C_SH1 * x;
-                dx = -C_SH1 * S(3);
-                dy = -C_SH1 * S(1);
-                dz = C_SH1 * S(2);
-                if (deg > 1) {
-                    const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-                    bas[4] = C_SH2[0] * xy;
-                    bas[5] = C_SH2[1] * yz;
-                    bas[6] = C_SH2[2] * (2.f * zz - xx - yy);
-                    bas[7] = C_SH2[3] * xz;
-                    bas[8] = C_SH2[4] * (xx - yy);
-                    dx = dx + (C_SH2[0] * y * S(4) + C_SH2[2] * 2.f * -x * S(6) + C_SH2[3] * z * S(7) +
-                               C_SH2[4] * 2.f * x * S(8));
-                    dy = dy + (C_SH2[0] * x * S(4) + C_SH2[1] * z * S(5) + C_SH2[2] * 2.f * -y * S(6) +
-                               C_SH2[4] * 2.f * -y * S(8));
-                    dz = dz + (C_SH2[1] * y * S(5) + C_SH2[2] * 2.f * 2.f * z * S(6) + C_SH2[3] * x * S(7));
-                    if (deg > 2) {
-                        bas[9] = C_SH3[0] * y * (3.f * xx - yy);
-                        bas[10] = C_SH3[1] * xy * z;
-                        bas[11] = C_SH3[2] * y * (4.f * zz - xx - yy);
-                        bas[12] = C_SH3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                        bas[13] = C_SH3[4] * x * (4.f * zz - xx - yy);
-                        bas[14] = C_SH3[5] * z * (xx - yy);
-                        bas[15] = C_SH3[6] * x * (xx - 3.f * yy);
-                        dx = dx + (C_SH3[0] * S(9) * 3.f * 2.f * xy + C_SH3[1] * S(10) * yz +
-                                   C_SH3[2] * S(11) * -2.f * xy + C_SH3[3] * S(12) * -3.f * 2.f * xz +
-                                   C_SH3[4] * S(13) * (-3.f * xx + 4.f * zz - yy) + C_SH3[5] * S(14) * 2.f * xz +
-                                   C_SH3[6] * S(15) * 3.f * (xx - yy));
-                        dy = dy + (C_SH3[0] * S(9) * 3.f * (xx - yy) + C_SH3[1] * S(10) * xz +
-                                   C_SH3[2] * S(11) * (-3.f * yy + 4.f * zz - xx) + C_SH3[3] * S(12) * -3.f * 2.f * yz +
-                                   C_SH3[4] * S(13) * -2.f * xy + C_SH3[5] * S(14) * -2.f * yz +
-                                   C_SH3[6] * S(15) * -3.f * 2.f * xy);
-                        dz = dz + (C_SH3[1] * S(10) * xy + C_SH3[2] * S(11) * 4.f * 2.f * yz +
-                                   C_SH3[3] * S(12) * 3.f * (2.f * zz - xx - yy) + C_SH3[4] * S(13) * 4.f * 2.f * xz +
-                                   C_SH3[5] * S(14) * (xx - yy));
-                    }
-                }
+                const float* J = jac_row(shjac, idx);
+                dx = {J[0], J[64], J[128]};
+                dy = {J[192], J[256], J[320]};
+                dz = {J[384], J[448], J[512]};
             }
+            // dL/dsh[i] = basis_i * dRGB (backward.cu:46-110); coefficients >= (D+1)^2 get 0
+            sh_basis(deg, dir, bas);
             dc[0] = dRGB.x;
             dc[1] = dRGB.y;
             dc[2] = dRGB.z;
@@ -1072,11 +1155,11 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv_sh(int P, int D, i
 
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec, int* radii,
                        uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped, ushort4* rect,
-                       uint32_t* rect32, void* zero_a, size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes,
+                       uint32_t* rect32, float* shjac, void* zero_a, size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes,
                        hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_preprocess, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, gx, gy, rec, radii,
-                       tiles_touched, depth_keys, clamped, rect, rect32, zero_a, cdiv(zero_a_bytes, 16), zero_b,
+                       tiles_touched, depth_keys, clamped, rect, rect32, shjac, zero_a, cdiv(zero_a_bytes, 16), zero_b,
                        cdiv(zero_b_bytes, 16));
 }
 
@@ -1111,11 +1194,11 @@ void launch_sh_backward(int P, int D, int M, const float* shs, const float* mean
 
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const uint32_t* written, const float4* rec,
-                              const gsr_grads& g, hipStream_t st) {
+                              const float* contrib, const uint8_t* written, const float4* rec,
+                              const float* shjac, const gsr_grads& g, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_gaussian_backward, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, radii, tiles_touched,
-                       goff, clamped, contrib, written, rec, g);
+                       goff, clamped, contrib, written, rec, shjac, g);
 }
 
 }  // namespace gsr

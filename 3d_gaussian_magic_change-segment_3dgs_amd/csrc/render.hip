@@ -23,7 +23,7 @@
 // gradient channels with a transposed butterfly on v_permlane32_swap /
 // v_permlane16_swap / DPP (34 VALU ops, no LDS round trips), and 12 lanes
 // store ONE 48-B record per replayed (tile, Gaussian) instance at the
-// instance's slot and set the slot's bit in a written-mask.  Instances that no
+// instance's slot and set the slot's byte in a written-flag array.  Instances that no
 // pixel replays (behind every last contributor, or out of reach) write nothing.
 // The per-Gaussian backward kernel sums a Gaussian's written slots in slot
 // order: deterministic, atomic-free gradients.  Record (q = G * dL_dalpha per pixel,
@@ -72,10 +72,32 @@ __device__ __forceinline__ float gsr_expf(float x) {
     const float scale = __uint_as_float((__float_as_uint(kf) << 23) + 0x3f800000u);
     return p * scale;
 }
+// gsr_expf without the clamp, for lanes whose argument is known to lie in [-87, 88]: the
+// blend loops call it only under a lane mask of pixels with power >= the Gaussian's
+// opacity floor (>= -5.6) and use the result only under that mask (other lanes get a
+// meaningless, possibly non-finite value that every use masks out).  Same bits as
+// gsr_expf on that range.
+__device__ __forceinline__ float gsr_expf_nc(float x) {
+    const float kf = __builtin_fmaf(x, 1.44269502f, 12582912.0f);
+    const float k = kf - 12582912.0f;
+    float r = __builtin_fmaf(-k, 0.693145751953125f, x);
+    r = __builtin_fmaf(-k, 1.42860677e-06f, r);
+    float p = 0.001381461275741458f;
+    p = __builtin_fmaf(p, r, 0.008368710055947304f);
+    p = __builtin_fmaf(p, r, 0.04166838899254799f);
+    p = __builtin_fmaf(p, r, 0.1666652113199234f);
+    p = __builtin_fmaf(p, r, 0.4999999403953552f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    p = __builtin_fmaf(p, r, 1.0f);
+    const float scale = __uint_as_float((__float_as_uint(kf) << 23) + 0x3f800000u);
+    return p * scale;
+}
 #ifdef GSR_FAST_EXP
 #define GSR_EXP(x) __expf(x)
+#define GSR_EXP_NC(x) __expf(x)
 #else
 #define GSR_EXP(x) gsr_expf(x)
+#define GSR_EXP_NC(x) gsr_expf_nc(x)
 #endif
 
 // Two pixels' powers at once: v_pk_add_f32 / v_pk_mul_f32 issue both elements for the
@@ -252,7 +274,8 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
             uint64_t near[4];  // per quadrant: live lanes within reach
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                power[k] = -0.5f * (ax[k & 1] + cy[k >> 1]) - bx[k & 1] * dyv[k >> 1];
+                // -0.5 S is exact, so -(0.5 S) - B as one fma(-0.5, S, -B): the same bits
+                power[k] = __builtin_fmaf(-0.5f, ax[k & 1] + cy[k >> 1], -(bx[k & 1] * dyv[k >> 1]));
                 near[k] = __builtin_amdgcn_ballot_w64(power[k] >= pm) & live[k];
             }
             STAT(0, 1);
@@ -264,21 +287,26 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
             const float4 q2 = srec[j][2], q3 = srec[j][3];
             const float op = q1.z, dep = q3.x, s0 = q1.w;
             const float cr = q2.x, cg = q2.y, cbl = q2.z, s1 = q2.w;
-            const uint32_t contributor = (uint32_t)(base + j + 1);
+            // in a VGPR once per pair: the per-quadrant v_cndmask below may read only one SGPR
+            // (its lane mask), so a scalar contributor would be re-moved into a VGPR per quadrant
+            uint32_t contributor = (uint32_t)(base + j + 1);
+            asm volatile("" : "+v"(contributor));
             // Quadrant k is blended only if one of its pixels can pass; the exact
             // reference tests below decide per pixel.
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (!near[k]) continue;
                 STAT(8, 1);
-                const bool lv = __builtin_amdgcn_inverse_ballot_w64(live[k]);
-                const float alpha = fminf(0.99f, op * GSR_EXP(power[k]));
-                const bool o = lv & (power[k] <= 0.0f) & (alpha >= ALPHA_MIN);
+                // lanes of near[k] (live, power >= the opacity floor) are the only ones that
+                // can pass; every result below is used only under that mask
+                const float alpha = fminf(0.99f, op * GSR_EXP_NC(power[k]));
+                const uint64_t m_o = near[k] & __builtin_amdgcn_ballot_w64(power[k] <= 0.0f) &
+                                     __builtin_amdgcn_ballot_w64(alpha >= ALPHA_MIN);
                 const float test_T = T[k] * (1.f - alpha);
-                const bool enough = test_T >= T_MIN;
-                const bool ok = o & enough;
+                const uint64_t m_done = m_o & __builtin_amdgcn_ballot_w64(test_T < T_MIN);  // forward.cu:355-357
+                live[k] &= ~m_done;
+                const bool ok = __builtin_amdgcn_inverse_ballot_w64(m_o & ~m_done);
                 STAT(4, POPC(ok));
-                live[k] &= ~__builtin_amdgcn_ballot_w64(o & !enough);  // terminated (forward.cu:355-357)
                 const float aT = (ok ? alpha : 0.f) * T[k];
                 C0[k] = __builtin_fmaf(cr, aT, C0[k]);
                 C1[k] = __builtin_fmaf(cg, aT, C1[k]);
@@ -384,7 +412,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                                                    const float* __restrict__ dL_dsegs,
                                                    const float* __restrict__ dL_ddepths,
                                                    const float* __restrict__ dL_dalphas,
-                                                   float* __restrict__ contrib, uint32_t* __restrict__ written) {
+                                                   float* __restrict__ contrib, uint8_t* __restrict__ written) {
 #pragma clang fp contract(off)
     const int tile = (int)order[blockIdx.x];
     const int lane = threadIdx.x;
@@ -505,7 +533,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                 for (int k = 0; k < 4; ++k) {
                     const float dy = gy_ - pfy[k];
                     dys[k] = dy;
-                    power[k] = -0.5f * (adxdx + cc * dy * dy) - bdx * dy;
+                    power[k] = __builtin_fmaf(-0.5f, adxdx + cc * dy * dy, -(bdx * dy));  // == -0.5 S - B
                     near[k] = __builtin_amdgcn_ballot_w64(p < lastc[k]) & __builtin_amdgcn_ballot_w64(power[k] >= pm);
                 }
                 STAT(0, 1);
@@ -527,26 +555,29 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                 for (int k = 0; k < 4; ++k) {
                     if (!near[k]) continue;
                     STAT(8, 1);
-                    const float G = GSR_EXP(power[k]);
+                    // near[k]: lanes replaying p (p < n_contrib) within reach (power >= the
+                    // opacity floor); G is used only under o, a subset of near[k]
+                    const float G = GSR_EXP_NC(power[k]);
                     const float a = fminf(0.99f, op * G);
-                    const bool o = (p < lastc[k]) & (power[k] <= 0.0f) & (a >= ALPHA_MIN);
+                    const bool o = __builtin_amdgcn_inverse_ballot_w64(
+                        near[k] & __builtin_amdgcn_ballot_w64(power[k] <= 0.0f) &
+                        __builtin_amdgcn_ballot_w64(a >= ALPHA_MIN));
                     STAT(4, POPC(o));
                     const float one_m = 1.f - a;
                     const float Tn = fdiv(T[k], one_m);
                     // a_m = alpha of a replayed pair, else 0: it masks dch and the Dk fold
                     const float a_m = o ? a : 0.f;
                     const float dch_m = a_m * Tn;
-                    float cdot = c0 * dp0[k];
+                    float cdot = __builtin_fmaf(c0, dp0[k], da[k]);  // alpha channel (colour 1) first
                     cdot = __builtin_fmaf(c1, dp1[k], cdot);
                     cdot = __builtin_fmaf(c2, dp2[k], cdot);
                     cdot = __builtin_fmaf(s0, ds0[k], cdot);
                     cdot = __builtin_fmaf(s1, ds1[k], cdot);
                     cdot = __builtin_fmaf(dep, dd[k], cdot);
-                    cdot += da[k];
                     const float diff = cdot - Dk[k];
                     float dopa = diff * Tn;
                     if (UB) dopa += (-Tfin[k] * __builtin_amdgcn_rcpf(one_m)) * bgdot[k];
-                    const float dopa_m = o ? dopa : 0.f;
+
                     acc[0] = __builtin_fmaf(dch_m, dp0[k], acc[0]);
                     acc[1] = __builtin_fmaf(dch_m, dp1[k], acc[1]);
                     acc[2] = __builtin_fmaf(dch_m, dp2[k], acc[2]);
@@ -557,7 +588,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                     // mean2D / conic terms (backward.cu:612-631) are op * q times a
                     // polynomial in (dx, dy) with per-Gaussian coefficients, so only the
                     // moments of q are summed here (see the record layout above).
-                    const float qg = G * dopa_m;
+                    const float qg = o ? G * dopa : 0.f;  // select after the product: G may be non-finite off o
                     const float qdy = qg * dys[k];
                     acc[6] += qg;
                     acc[8] += qdy;
@@ -574,8 +605,9 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                 bool valid;
                 const float r = wave_reduce12(acc, lane, vidx, valid);
                 if (valid) dst[vidx] = r;
-                // Bit u marks slot u as written (order-independent OR: deterministic).
-                if (lane == 0) atomicOr(&written[u >> 5], 1u << (u & 31));
+                // Byte u marks slot u as written: one plain store of one byte by the whole
+                // wave (a uniform address; no atomic, no lane election).
+                written[u] = 1;
             }
         }
     };
@@ -602,7 +634,7 @@ void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order,
                             const uint32_t* point_list, const uint32_t* slot_vals, const float4* rec,
                             const float* bg, const float* alpha, const uint32_t* n_contrib, const float* dL_dcolor,
                             const float* dL_dsegment, const float* dL_ddepth, const float* dL_dalpha, float* contrib,
-                            uint32_t* written, hipStream_t st) {
+                            uint8_t* written, hipStream_t st) {
     const int T = gx * gy;
     if (T == 0) return;
     hipLaunchKernelGGL(k_render_bwd, dim3(T), dim3(64), 0, st, W, H, gx, order, ranges, point_list, slot_vals, rec,

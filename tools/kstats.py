@@ -1,0 +1,14 @@
+"""Summarise a rocprofv3 kernel_stats.csv: one line per gsr kernel (short name, calls, avg/min/max us)."""
+import csv
+import re
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+for r in rows:
+    n = r["Name"]
+    if "at::" in n and "--all" not in sys.argv:
+        continue
+    m = re.search(r"(k_[A-Za-z0-9_]+)(<[^>]*>)?", n)
+    short = (m.group(1) + (m.group(2) or "")) if m else n[:50]
+    print(f"{short:44s} calls={r['Calls']:>5s} avg_us={float(r['AverageNs']) / 1e3:8.2f} "
+          f"min={float(r['MinNs']) / 1e3:8.2f} max={float(r['MaxNs']) / 1e3:8.2f}")
