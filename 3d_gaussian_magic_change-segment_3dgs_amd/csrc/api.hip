@@ -188,10 +188,15 @@ const char* gsr_last_error(void) { return g_last_error.c_str(); }
 const char* gsr_version(void) { return "gsr 0.1 (gfx950)"; }
 
 static bool g_speculate = getenv("GSR_SPECULATE") == nullptr || getenv("GSR_SPECULATE")[0] != '0';
+static bool g_rows_binning = getenv("GSR_ROWS_BINNING") == nullptr || getenv("GSR_ROWS_BINNING")[0] != '0';
 int gsr_set_option(const char* name, long long value) {
     if (!name) return fail("[gsr] option name is NULL");
     if (std::string(name) == "speculate") {  // gsr_forward's speculative stage B (default on)
         g_speculate = value != 0;
+        return 0;
+    }
+    if (std::string(name) == "rows_binning") {  // binning_rows.hip for grids <= 255 x 255 tiles (default on)
+        g_rows_binning = value != 0;
         return 0;
     }
     if (std::string(name) == "sort_lookback_max") {
@@ -334,41 +339,72 @@ int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* b
     const BinLayout BL = bin_layout(cap);
     char* b = I > 0 ? aligned_base(binning) : nullptr;
     uint32_t* point_list = nullptr;
+    uint32_t* order = at<uint32_t>(im, IL.order);
+    const bool rows = I > 0 && g_rows_binning && rect_packable(IL.gx, IL.gy);
     if (I > 0) {
         if (!geom || !binning) return fail("[gsr] geom/binning buffers are NULL");
-        {
-            StageScope sc(GSR_STAGE_DUPLICATE, st);
-            launch_duplicate(P, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets),
-                             at<uint32_t>(g, GL.tiles_touched), at<ushort4>(g, GL.rect),
-                             rect_packable(IL.gx, IL.gy) ? at<uint32_t>(g, GL.rect32_sorted) : nullptr, IL.gx,
-                             at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid), at<uint32_t>(g, GL.goff),
-                             ranges, T, (uint32_t)cap, st);
+        if (rows) {
+            // tile lists by row-then-tile expansion of the depth-ordered Gaussians
+            // (binning_rows.hip): level 1 under the "duplicate" stage, level 2 under
+            // "tile_sort", ranges + tile order under "ranges"
+            const uint32_t* n_total = at<uint32_t>(g, GL.offsets) + (P - 1);
+            auto rb = [&](int stage) {
+                launch_rows_binning(P, IL.gx, IL.gy, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets),
+                                    at<uint32_t>(g, GL.rect32_sorted), at<uint32_t>(g, GL.goff), g + GL.ws, b + BL.ws,
+                                    at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.tkeys_alt),
+                                    at<uint32_t>(b, BL.vals_alt), at<uint32_t>(b, BL.point_list),
+                                    at<uint32_t>(b, BL.slot_vals), ranges, order, at<uint4>(b, BL.written),
+                                    cdiv(cap, 16), cap, n_total, st, stage);
+            };
+            {
+                StageScope sc(GSR_STAGE_DUPLICATE, st);
+                rb(0);
+            }
+            GSR_STAGE("rows");
+            {
+                StageScope sc(GSR_STAGE_TILE_SORT, st);
+                rb(1);
+            }
+            GSR_STAGE("tiles");
+            {
+                StageScope sc(GSR_STAGE_RANGES, st);
+                rb(2);
+            }
+            GSR_STAGE("tile ranges + order");
+        } else {
+            {
+                StageScope sc(GSR_STAGE_DUPLICATE, st);
+                launch_duplicate(P, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets),
+                                 at<uint32_t>(g, GL.tiles_touched), at<ushort4>(g, GL.rect),
+                                 rect_packable(IL.gx, IL.gy) ? at<uint32_t>(g, GL.rect32_sorted) : nullptr, IL.gx,
+                                 at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid), at<uint32_t>(g, GL.goff),
+                                 ranges, T, (uint32_t)cap, st);
+            }
+            GSR_STAGE("duplicate");
+            const int bits = (int)higher_msb((uint32_t)T);
+            const int passes = (bits + RADIX_BITS - 1) / RADIX_BITS;
+            // even pass count: sorted keys return to tkeys; odd: they land in tkeys_alt.
+            uint32_t* kin = at<uint32_t>(b, BL.tkeys);
+            uint32_t* kalt = at<uint32_t>(b, BL.tkeys_alt);
+            uint32_t* kout = (passes % 2 == 0) ? kin : kalt;
+            uint32_t* ktmp = (passes % 2 == 0) ? kalt : kin;
+            {
+                // key = tile, payload = (instance slot u, Gaussian id): the slot orders ties by
+                // (depth, gaussian); the id travels along so point_list needs no gather.
+                StageScope sc(GSR_STAGE_TILE_SORT, st);
+                // the last pass also produces the tile ranges (identifyTileRanges,
+                // rasterizer_impl.cu:113-138) and clears the backward's written-slot flags
+                const SortFinal fin{ranges, at<uint4>(b, BL.written), cdiv(cap, 16)};
+                launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout,
+                                  at<uint32_t>(b, BL.slot_vals), I, bits, b + BL.ws, /*ws_zeroed=*/false, st,
+                                  at<uint32_t>(b, BL.slot_gid), at<uint32_t>(b, BL.gid_alt),
+                                  at<uint32_t>(b, BL.point_list), &fin, /*skip_sentinel=*/false, n_dev);
+            }
+            GSR_STAGE("tile sort");
         }
-        GSR_STAGE("duplicate");
-        const int bits = (int)higher_msb((uint32_t)T);
-        const int passes = (bits + RADIX_BITS - 1) / RADIX_BITS;
-        // even pass count: sorted keys return to tkeys; odd: they land in tkeys_alt.
-        uint32_t* kin = at<uint32_t>(b, BL.tkeys);
-        uint32_t* kalt = at<uint32_t>(b, BL.tkeys_alt);
-        uint32_t* kout = (passes % 2 == 0) ? kin : kalt;
-        uint32_t* ktmp = (passes % 2 == 0) ? kalt : kin;
-        {
-            // key = tile, payload = (instance slot u, Gaussian id): the slot orders ties by
-            // (depth, gaussian); the id travels along so point_list needs no gather.
-            StageScope sc(GSR_STAGE_TILE_SORT, st);
-            // the last pass also produces the tile ranges (identifyTileRanges,
-            // rasterizer_impl.cu:113-138) and clears the backward's written-slot mask
-            const SortFinal fin{ranges, at<uint4>(b, BL.written), cdiv(I, 16)};
-            launch_radix_sort(kin, nullptr, ktmp, at<uint32_t>(b, BL.vals_alt), kout, at<uint32_t>(b, BL.slot_vals),
-                              I, bits, b + BL.ws, /*ws_zeroed=*/false, st,
-                              at<uint32_t>(b, BL.slot_gid), at<uint32_t>(b, BL.gid_alt),
-                              at<uint32_t>(b, BL.point_list), &fin, /*skip_sentinel=*/false, n_dev);
-        }
-        GSR_STAGE("tile sort");
         point_list = at<uint32_t>(b, BL.point_list);
     }
-    uint32_t* order = at<uint32_t>(im, IL.order);
-    {
+    if (!rows) {
         StageScope sc(GSR_STAGE_RANGES, st);
         launch_tile_order(ranges, T, order, st);
     }

@@ -174,16 +174,21 @@ __device__ __forceinline__ uint32_t block_exclusive_scan_w(uint32_t v, uint32_t*
 // out[i] = sum_{j<=i (INCLUSIVE) / j<i} value(j), value(j) = gather ? src[gather[j]] : src[j], in one
 // pass: each tile of 4096 values is staged through LDS (coalesced loads/stores),
 // reduced, its prefix found by look-back, then scanned.
+// n_dev (optional): a device word; the scan then covers min(n, *n_dev) values (n sizes the
+// grid; tiles past the device count return at once -- no later tile depends on them).
 template <bool INCLUSIVE>
 __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restrict__ src,
                                                        const uint32_t* __restrict__ gather, size_t n,
                                                        uint32_t* __restrict__ out, uint64_t* status,
-                                                       uint32_t* counter, uint32_t* host_total, int rect_mode) {
+                                                       uint32_t* counter, uint32_t* host_total, int rect_mode,
+                                                       const uint32_t* n_dev) {
     __shared__ uint32_t tile[SCAN_TILE + SCAN_TILE / 32];
     __shared__ uint32_t wsum[4];
     __shared__ uint32_t s_excl;
+    if (n_dev) n = min(n, (size_t)*n_dev);
     const int t = lb_tile_index(counter);
     const size_t base = (size_t)t * SCAN_TILE;
+    if (base >= n && t > 0) return;  // uniform: past the device count
     auto pad = [](int i) { return i + (i >> 5); };
     uint32_t v[SCAN_ITEMS], sum = 0;
     if (gather) {
@@ -665,7 +670,7 @@ void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_id
     const ScanWs W = scan_ws(n, ws);
     if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, W.bytes, st);
     hipLaunchKernelGGL(k_scan<true>, dim3(cdiv(n, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, src, gather_idx, n, out,
-                       W.status, W.counter, host_total, (int)rect_mode);
+                       W.status, W.counter, host_total, (int)rect_mode, nullptr);
 }
 
 // Sorting modes (measured on MI355X): small sorts are launch-bound and use one
@@ -753,7 +758,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
                                kin, n, shift,
                                bits, W.table, S.base, cdiv(S.bytes, 16), n_dev);
             hipLaunchKernelGGL(k_scan<false>, dim3(cdiv(len, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, W.table,
-                               nullptr, len, W.table, S.status, S.counter, nullptr, 0);
+                               nullptr, len, W.table, S.status, S.counter, nullptr, 0, nullptr);
             launch_scatter<GSR_TB_ITEMS, GSR_TB_WAVES, false>(n, kin, vin, kout, vout, shift, bits, W.table, nullptr,
                                                               nullptr, v2in, v2out, fin, nullptr, n_dev, st);
         }
@@ -761,6 +766,13 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
         vin = vout;
         v2in = v2out;
     }
+}
+
+void launch_scan_exclusive(const uint32_t* src, uint32_t* out, size_t n, const uint32_t* n_dev, const ScanWs& W,
+                           hipStream_t st) {
+    if (n == 0) return;
+    hipLaunchKernelGGL(k_scan<false>, dim3(cdiv(n, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, src, nullptr, n, out,
+                       W.status, W.counter, nullptr, 0, n_dev);
 }
 
 void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st) {

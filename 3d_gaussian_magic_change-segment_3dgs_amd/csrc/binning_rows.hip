@@ -1,0 +1,433 @@
+// binning_rows.hip -- per-tile instance lists by two stable expansions of the
+// depth-ordered Gaussians, rows first, then tiles.  Replaces, for grids of up to
+// 255 x 255 tiles (4080 x 4080 px), the reference's duplicateWithKeys +
+// DeviceRadixSort::SortPairs + identifyTileRanges (DGR/cuda_rasterizer/
+// rasterizer_impl.cu:68-138, :291-322); wider grids keep binning.hip's duplicate + radix
+// sort.
+//
+// Input: the Gaussians in depth order r = 0..P-1 (binning.hip's depth sort): the id
+// order[r], the packed tile rectangle rect[r] = x0 | y0 << 8 | x1 << 16 | y1 << 24 and
+// the inclusive scan offsets[r] of the tile counts (the instance slots of r start at
+// offsets[r - 1]).  Output: point_list (Gaussian ids grouped by tile, by depth inside a
+// tile: the reference's sorted (tile << 32 | depth) order, bit for bit), slot_vals (each
+// entry's instance slot u = goff + (y - y0) w + (x - x0), the slot the backward's record
+// goes to), goff, ranges and the heavy-first tile order.
+//
+//   level 1 (rows):  Gaussian r -> one entry per tile row y0..y1-1 of its rectangle,
+//                    grouped by row, in depth order inside a row;
+//   level 2 (tiles): row entry -> one instance per tile x0..x1-1 of its row, grouped by
+//                    tile, in depth order inside a tile.
+// Each level is a chunked stable counting sort (bucket = row, or tile column of the row):
+//   count:   per chunk of RB_CH items, the bucket histogram (a difference array in LDS:
+//            two atomics per item) -> table[bucket][chunk];
+//   scan:    one exclusive scan of the bucket-major table (k_scan) gives every
+//            (bucket, chunk) the position of its first item;
+//   scatter: the chunk marks in LDS, per bucket, the RB_CH-bit set of its items that
+//            cover the bucket; an item's rank in its bucket is the popcount of the set
+//            bits below its own (stable and deterministic, no ordered atomics); the
+//            chunk's output is assembled in LDS in bucket order and written as runs.
+// Level-2 chunks never straddle rows (row y's entries form ceil(R_y / RB_CH) chunks), so
+// a chunk's buckets are the gx columns of one row.  Bytes per instance: 8 written
+// (point_list, slot_vals) plus ~12 written and read per row entry (~2.9 instances each at
+// the metric scene), against ~52 for duplicate + two radix passes over (key, slot, id).
+#include "gsr_internal.h"
+
+namespace gsr {
+
+namespace {
+
+constexpr int RB_CH = 512;            // items per chunk = threads per block
+constexpr int RB_W = RB_CH / 32;      // bitmask words per bucket
+constexpr int RB_STAGE = 2048;        // outputs a chunk assembles in LDS (more: direct writes)
+constexpr int RB_MAXB = 256;          // buckets per chunk (<= 255 rows / columns)
+constexpr int RB_GRID2 = 2048;        // blocks of the level-2 kernels (grid-stride over chunks)
+
+// Exclusive scan of n <= 256 LDS values v[0..n) by wave 0 (4 values per lane): out[k] =
+// sum of v[0..k); *tot = sum of all.  Every thread of the block must call it (barrier).
+__device__ void lds_scan256(const uint32_t* v, int n, uint32_t* out, uint32_t* tot) {
+    if (threadIdx.x < 64) {
+        const int l = threadIdx.x;
+        uint32_t a[4], s = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = 4 * l + i;
+            a[i] = k < n ? v[k] : 0u;
+            s += a[i];
+        }
+        uint32_t x = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if (l >= o) x += y;
+        }
+        uint32_t e = x - s;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int k = 4 * l + i;
+            if (k < n) out[k] = e;
+            e += a[i];
+        }
+        if (l == 63) *tot = x;
+    }
+    __syncthreads();
+}
+
+// bits[b * RB_W + w]: bit i of word w = item 32 w + i of the chunk covers bucket b.
+// pre[b * RB_W + w] = items of bucket b in words < w; cnt[b] = items of bucket b.
+__device__ void bucket_prefix(const uint32_t* bits, int nb, uint32_t* pre, uint32_t* cnt) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int PER_WAVE = 64 / RB_W;  // buckets per wave pass
+    for (int b0 = PER_WAVE * wave; b0 < nb; b0 += PER_WAVE * (RB_CH / 64)) {
+        const int b = b0 + lane / RB_W, w = lane % RB_W;
+        const uint32_t c = b < nb ? (uint32_t)__popc(bits[b * RB_W + w]) : 0u;
+        uint32_t x = c;
+#pragma unroll
+        for (int o = 1; o < RB_W; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, RB_W);
+            if (w >= o) x += y;
+        }
+        if (b < nb) {
+            pre[b * RB_W + w] = x - c;
+            if (w == RB_W - 1) cnt[b] = x;
+        }
+    }
+    __syncthreads();
+}
+
+__device__ __forceinline__ void unpack_rect(uint32_t pr, int& x0, int& y0, int& x1, int& y1) {
+    x0 = (int)(pr & 255u);
+    y0 = (int)((pr >> 8) & 255u);
+    x1 = (int)((pr >> 16) & 255u);
+    y1 = (int)(pr >> 24);
+}
+
+// ---------------------------------------------------------------- level 1 --
+// table1[y * nch1 + c] = Gaussians of chunk c (RB_CH depth-ordered Gaussians) covering row y.
+__global__ void __launch_bounds__(RB_CH) k_rows_count(int P, int gy, int nch1, const uint32_t* __restrict__ rect,
+                                                      uint32_t* __restrict__ table1, void* zero, size_t nzero16) {
+    __shared__ int d[RB_MAXB + 1];
+    __shared__ uint32_t e[RB_MAXB + 1];
+    __shared__ uint32_t tot;
+    zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH + threadIdx.x, (size_t)gridDim.x * RB_CH);  // scan-1 words
+    for (int i = threadIdx.x; i <= gy; i += RB_CH) d[i] = 0;
+    __syncthreads();
+    const int r = blockIdx.x * RB_CH + threadIdx.x;
+    if (r < P) {
+        int x0, y0, x1, y1;
+        unpack_rect(rect[r], x0, y0, x1, y1);
+        if (x1 > x0 && y1 > y0) {
+            atomicAdd(&d[y0], 1);
+            atomicAdd(&d[y1], -1);
+        }
+    }
+    __syncthreads();
+    lds_scan256(reinterpret_cast<const uint32_t*>(d), gy + 1, e, &tot);  // e[y + 1] = rows' counts
+    for (int y = threadIdx.x; y < gy; y += RB_CH) table1[(size_t)y * nch1 + blockIdx.x] = e[y + 1];
+}
+
+// Level-1 entries (E1, grouped by row): e_gid = Gaussian id, e_u = its first instance slot
+// in the row, e_x = x0 | x1 << 8.  Also goff[gid] (the backward's record slots).
+// Dynamic LDS: bits + pre, 2 x gy x RB_W words (sized by the grid, not the 255 bound:
+// four blocks per CU at 1080p).  Every global load is issued before the first barrier.
+__global__ void __launch_bounds__(RB_CH) k_rows_scatter(int P, int gy, int nch1, const uint32_t* __restrict__ order,
+                                                        const uint32_t* __restrict__ offsets,
+                                                        const uint32_t* __restrict__ rect,
+                                                        const uint32_t* __restrict__ base1, uint32_t* __restrict__ goff,
+                                                        uint32_t* __restrict__ e_gid, uint32_t* __restrict__ e_u,
+                                                        uint32_t* __restrict__ e_x, uint32_t cap) {
+    extern __shared__ uint32_t dyn[];
+    uint32_t* bits = dyn;
+    uint32_t* pre = dyn + gy * RB_W;
+    __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
+    __shared__ uint32_t s_gid[RB_STAGE], s_u[RB_STAGE], s_x[RB_STAGE];
+    __shared__ uint32_t tot;
+    const int tid = threadIdx.x;
+    const int r = blockIdx.x * RB_CH + tid;
+    int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
+    uint32_t g = 0, off = 0;
+    if (r < P) {
+        unpack_rect(rect[r], x0, y0, x1, y1);
+        g = order[r];
+        off = r == 0 ? 0u : offsets[r - 1];
+    }
+    for (int i = tid; i < gy * RB_W; i += RB_CH) bits[i] = 0;
+    for (int y = tid; y < gy; y += RB_CH) gb[y] = base1[(size_t)y * nch1 + blockIdx.x];
+    __syncthreads();
+    const bool vis = x1 > x0 && y1 > y0;
+    const uint32_t bit = 1u << (tid & 31), wd = (uint32_t)tid >> 5;
+    if (vis)
+        for (int y = y0; y < y1; ++y) atomicOr(&bits[y * RB_W + wd], bit);
+    __syncthreads();
+    bucket_prefix(bits, gy, pre, cnt);
+    lds_scan256(cnt, gy, lst, &tot);
+    const bool staged = tot <= (uint32_t)RB_STAGE;  // uniform
+    if (vis) {
+        goff[g] = off;
+        const uint32_t w = (uint32_t)(x1 - x0), below = bit - 1u;
+        for (int y = y0; y < y1; ++y) {
+            const uint32_t rank = pre[y * RB_W + wd] + (uint32_t)__popc(bits[y * RB_W + wd] & below);
+            const uint32_t u = off + (uint32_t)(y - y0) * w;
+            const uint32_t xr = (uint32_t)x0 | ((uint32_t)x1 << 8) | ((uint32_t)y << 16);
+            if (staged) {
+                const uint32_t lp = lst[y] + rank;
+                s_gid[lp] = g;
+                s_u[lp] = u;
+                s_x[lp] = xr;
+            } else {
+                const uint32_t gp = gb[y] + rank;
+                if (gp < cap) {
+                    e_gid[gp] = g;
+                    e_u[gp] = u;
+                    e_x[gp] = xr & 0xFFFFu;
+                }
+            }
+        }
+    }
+    if (!staged) return;
+    __syncthreads();
+    for (uint32_t i = tid; i < tot; i += RB_CH) {
+        const uint32_t xr = s_x[i], y = xr >> 16;
+        const uint32_t gp = gb[y] + (i - lst[y]);
+        if (gp < cap) {
+            e_gid[gp] = s_gid[i];
+            e_u[gp] = s_u[i];
+            e_x[gp] = xr & 0xFFFFu;
+        }
+    }
+}
+
+// ---------------------------------------------------------------- level 2 --
+// Row map of the level-2 chunks from the level-1 table: rs[y] = first entry of row y
+// (rs[gy] = entries), nsub[y] = chunks of row y, c0[y] = first chunk of row y; returns the
+// number of chunks.  Clamped to the entry capacity (a speculative stage B whose
+// num_rendered exceeds the buffer writes nothing past it; its results are discarded).
+struct RowMap {
+    uint32_t rs[RB_MAXB + 1], nsub[RB_MAXB + 1], c0[RB_MAXB + 1], nch2;
+};
+__device__ void build_row_map(RowMap& m, int gy, int nch1, const uint32_t* table1, const uint32_t* base1,
+                              uint32_t cap) {
+    const int tid = threadIdx.x;
+    for (int y = tid; y < gy; y += blockDim.x) m.rs[y] = min(base1[(size_t)y * nch1], cap);
+    if (tid == 0) {
+        const size_t last = (size_t)gy * nch1 - 1;
+        m.rs[gy] = min(base1[last] + table1[last], cap);
+    }
+    __syncthreads();
+    for (int y = tid; y < gy; y += blockDim.x) m.nsub[y] = (uint32_t)cdiv(m.rs[y + 1] - m.rs[y], RB_CH);
+    __syncthreads();
+    lds_scan256(m.nsub, gy, m.c0, &m.nch2);
+    if (tid == 0) m.c0[gy] = m.nch2;
+    __syncthreads();
+}
+// row of chunk c (< nch2): the last row y with c0[y] <= c
+__device__ __forceinline__ int chunk_row(const RowMap& m, int gy, uint32_t c) {
+    int lo = 0, hi = gy;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (m.c0[mid] <= c) lo = mid; else hi = mid - 1;
+    }
+    return lo;
+}
+__device__ __forceinline__ size_t tile_slot(const RowMap& m, int gx, int y, int x, uint32_t s) {
+    return (size_t)gx * m.c0[y] + (size_t)x * m.nsub[y] + s;  // (row, column, sub-chunk) order
+}
+
+// table2[tile_slot(y, x, s)] = entries of sub-chunk s of row y covering column x.
+// Also clears the tile ranges (rows without entries keep {0, 0}: rasterizer_impl.cu:316).
+__global__ void __launch_bounds__(RB_CH) k_tiles_count(int gx, int gy, int nch1, const uint32_t* __restrict__ table1,
+                                                       const uint32_t* __restrict__ base1,
+                                                       const uint32_t* __restrict__ e_x, uint32_t* __restrict__ table2,
+                                                       uint32_t* __restrict__ len2, uint32_t cap, void* zero,
+                                                       size_t nzero16, uint2* __restrict__ ranges) {
+    __shared__ RowMap m;
+    __shared__ int d[RB_MAXB + 1];
+    __shared__ uint32_t e[RB_MAXB + 1];
+    __shared__ uint32_t tot;
+    zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH + threadIdx.x, (size_t)gridDim.x * RB_CH);  // scan-2 words
+    for (int t = blockIdx.x * RB_CH + threadIdx.x; t < gx * gy; t += gridDim.x * RB_CH) ranges[t] = make_uint2(0u, 0u);
+    build_row_map(m, gy, nch1, table1, base1, cap);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *len2 = (uint32_t)gx * m.nch2;
+    for (uint32_t c = blockIdx.x; c < m.nch2; c += gridDim.x) {
+        const int y = chunk_row(m, gy, c);
+        const uint32_t s = c - m.c0[y], e0 = m.rs[y] + s * RB_CH, n = min((uint32_t)RB_CH, m.rs[y + 1] - e0);
+        for (int i = threadIdx.x; i <= gx; i += RB_CH) d[i] = 0;
+        __syncthreads();
+        if (threadIdx.x < n) {
+            const uint32_t xr = e_x[e0 + threadIdx.x];
+            atomicAdd(&d[xr & 255u], 1);
+            atomicAdd(&d[(xr >> 8) & 255u], -1);
+        }
+        __syncthreads();
+        lds_scan256(reinterpret_cast<const uint32_t*>(d), gx + 1, e, &tot);  // e[x + 1] = column counts
+        for (int x = threadIdx.x; x < gx; x += RB_CH) table2[tile_slot(m, gx, y, x, s)] = e[x + 1];
+        __syncthreads();
+    }
+}
+
+// point_list / slot_vals; the ranges of every non-empty row (from the chunk s = 0 of the
+// row: the first entry of (y, x, 0) and of the next column, clamped to the capacity, empty
+// tiles {0, 0}); also clears the backward's written-slot flags.  The next chunk's entries
+// and bucket bases are loaded while the current one is ranked (software pipeline: a chunk
+// otherwise waits on two dependent global round trips).  Dynamic LDS: bits + pre,
+// 2 x gx x RB_W words.
+__global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch1, const uint32_t* __restrict__ table1,
+                                                         const uint32_t* __restrict__ base1,
+                                                         const uint32_t* __restrict__ base2,
+                                                         const uint32_t* __restrict__ e_gid,
+                                                         const uint32_t* __restrict__ e_u,
+                                                         const uint32_t* __restrict__ e_x,
+                                                         uint32_t* __restrict__ point_list,
+                                                         uint32_t* __restrict__ slot_vals, uint32_t cap,
+                                                         const uint32_t* __restrict__ n_total,
+                                                         uint2* __restrict__ ranges, uint4* zero, size_t nzero16) {
+    extern __shared__ uint32_t dyn[];
+    uint32_t* bits = dyn;
+    uint32_t* pre = dyn + gx * RB_W;
+    __shared__ RowMap m;
+    __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
+    __shared__ uint32_t s_gid[RB_STAGE], s_u[RB_STAGE];
+    __shared__ uint8_t s_x[RB_STAGE];
+    __shared__ uint32_t tot;
+    const int tid = threadIdx.x;
+    for (size_t i = (size_t)blockIdx.x * RB_CH + tid; i < nzero16; i += (size_t)gridDim.x * RB_CH)
+        zero[i] = make_uint4(0u, 0u, 0u, 0u);
+    build_row_map(m, gy, nch1, table1, base1, cap);
+    const uint32_t len2 = (uint32_t)gx * m.nch2, itot = min(*n_total, cap);
+    const uint32_t bit = 1u << (tid & 31), wd = (uint32_t)tid >> 5, below = bit - 1u;
+    // chunk c -> its row, sub-chunk, entries, this thread's entry and bucket base (prefetch)
+    struct Chunk {
+        int y;
+        uint32_t s, e0, n, g, u, xr, gbv;
+    };
+    auto fetch = [&](uint32_t c) {
+        Chunk k;
+        k.y = chunk_row(m, gy, c);
+        k.s = c - m.c0[k.y];
+        k.e0 = m.rs[k.y] + k.s * RB_CH;
+        k.n = min((uint32_t)RB_CH, m.rs[k.y + 1] - k.e0);
+        k.g = k.u = k.xr = 0;
+        if ((uint32_t)tid < k.n) {
+            k.g = e_gid[k.e0 + tid];
+            k.u = e_u[k.e0 + tid];
+            k.xr = e_x[k.e0 + tid];
+        }
+        k.gbv = tid < gx ? base2[tile_slot(m, gx, k.y, tid, k.s)] : 0u;
+        return k;
+    };
+    uint32_t c = blockIdx.x;
+    Chunk cur;
+    if (c < m.nch2) cur = fetch(c);
+    while (c < m.nch2) {
+        const int y = cur.y;
+        for (int i = tid; i < gx * RB_W; i += RB_CH) bits[i] = 0;
+        if (tid < gx) gb[tid] = cur.gbv;
+        __syncthreads();
+        const bool live = (uint32_t)tid < cur.n;
+        const int x0 = (int)(cur.xr & 255u), x1 = (int)((cur.xr >> 8) & 255u);
+        if (live)
+            for (int x = x0; x < x1; ++x) atomicOr(&bits[x * RB_W + wd], bit);
+        if (cur.s == 0 && tid < gx) {  // this row's tile ranges
+            const uint32_t a = min(gb[tid], cap);
+            uint32_t b;
+            if (tid + 1 < gx) {
+                b = base2[tile_slot(m, gx, y, tid + 1, 0)];
+            } else {
+                const size_t nx = (size_t)gx * m.c0[y + 1];
+                b = nx < len2 ? base2[nx] : itot;
+            }
+            b = min(b, cap);
+            ranges[(size_t)y * gx + tid] = b > a ? make_uint2(a, b) : make_uint2(0u, 0u);
+        }
+        const uint32_t cn = c + gridDim.x;
+        Chunk nxt;
+        if (cn < m.nch2) nxt = fetch(cn);  // in flight while this chunk is ranked
+        __syncthreads();
+        bucket_prefix(bits, gx, pre, cnt);
+        lds_scan256(cnt, gx, lst, &tot);
+        const bool staged = tot <= (uint32_t)RB_STAGE;  // uniform
+        if (live)
+            for (int x = x0; x < x1; ++x) {
+                const uint32_t rank = pre[x * RB_W + wd] + (uint32_t)__popc(bits[x * RB_W + wd] & below);
+                const uint32_t uu = cur.u + (uint32_t)(x - x0);
+                if (staged) {
+                    const uint32_t lp = lst[x] + rank;
+                    s_gid[lp] = cur.g;
+                    s_u[lp] = uu;
+                    s_x[lp] = (uint8_t)x;
+                } else {
+                    const uint32_t gp = gb[x] + rank;
+                    if (gp < cap) {
+                        point_list[gp] = cur.g;
+                        slot_vals[gp] = uu;
+                    }
+                }
+            }
+        if (staged) {
+            __syncthreads();
+            for (uint32_t i = tid; i < tot; i += RB_CH) {
+                const uint32_t x = s_x[i];
+                const uint32_t gp = gb[x] + (i - lst[x]);
+                if (gp < cap) {
+                    point_list[gp] = s_gid[i];
+                    slot_vals[gp] = s_u[i];
+                }
+            }
+        }
+        __syncthreads();
+        c = cn;
+        cur = nxt;
+    }
+}
+
+}  // namespace
+
+size_t rows_bin_geom_ws_bytes(size_t P, int gy) {
+    const size_t n1 = (size_t)gy * cdiv(P > 0 ? P : 1, RB_CH);
+    return 2 * align_up(n1 * 4) + scan_ws_bytes(n1);
+}
+
+size_t rows_bin_ws_bytes(size_t cap) {
+    const size_t n2 = (size_t)RB_MAXB * (RB_MAXB + cdiv(cap > 0 ? cap : 1, RB_CH));
+    return ALIGN + 2 * align_up(n2 * 4) + scan_ws_bytes(n2);
+}
+
+void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uint32_t* offsets, const uint32_t* rect,
+                         uint32_t* goff, void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_u, uint32_t* e_x,
+                         uint32_t* point_list, uint32_t* slot_vals, uint2* ranges, uint32_t* tile_order,
+                         uint4* written, size_t written16, size_t cap, const uint32_t* n_total, hipStream_t st,
+                         int stage) {
+    const int nch1 = (int)cdiv(P, RB_CH);
+    const size_t n1 = (size_t)gy * nch1;
+    char* gw = static_cast<char*>(geom_ws);
+    uint32_t* table1 = reinterpret_cast<uint32_t*>(gw);
+    uint32_t* base1 = reinterpret_cast<uint32_t*>(gw + align_up(n1 * 4));
+    void* scan1 = gw + 2 * align_up(n1 * 4);
+    const ScanWs S1 = scan_ws(n1, scan1);
+    const size_t n2 = (size_t)gx * (gy + cdiv(cap, RB_CH));  // table-2 entries bound
+    char* bw = static_cast<char*>(bin_ws);
+    uint32_t* len2 = reinterpret_cast<uint32_t*>(bw);
+    uint32_t* table2 = reinterpret_cast<uint32_t*>(bw + ALIGN);
+    uint32_t* base2 = reinterpret_cast<uint32_t*>(bw + ALIGN + align_up(n2 * 4));
+    void* scan2 = bw + ALIGN + 2 * align_up(n2 * 4);
+    const ScanWs S2 = scan_ws(n2, scan2);
+    const uint32_t cap32 = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
+    if (stage == 0) {  // level 1: rows
+        hipLaunchKernelGGL(k_rows_count, dim3(nch1), dim3(RB_CH), 0, st, P, gy, nch1, rect, table1, S1.base,
+                           cdiv(S1.bytes, 16));
+        launch_scan_exclusive(table1, base1, n1, nullptr, S1, st);
+        hipLaunchKernelGGL(k_rows_scatter, dim3(nch1), dim3(RB_CH), 2 * gy * RB_W * 4, st, P, gy, nch1, order,
+                           offsets, rect, base1, goff, e_gid, e_u, e_x, cap32);
+    } else if (stage == 1) {  // level 2: tiles (+ ranges)
+        const int grid2 = (int)std::min<size_t>(RB_GRID2, gy + cdiv(cap, RB_CH));
+        hipLaunchKernelGGL(k_tiles_count, dim3(grid2), dim3(RB_CH), 0, st, gx, gy, nch1, table1, base1, e_x, table2,
+                           len2, cap32, S2.base, cdiv(S2.bytes, 16), ranges);
+        launch_scan_exclusive(table2, base2, n2, len2, S2, st);
+        hipLaunchKernelGGL(k_tiles_scatter, dim3(grid2), dim3(RB_CH), 2 * gx * RB_W * 4, st, gx, gy, nch1, table1,
+                           base1, base2, e_gid, e_u, e_x, point_list, slot_vals, cap32, n_total, ranges, written,
+                           written16);
+    } else {  // heavy-first tile order (binning.hip)
+        launch_tile_order(ranges, gx * gy, tile_order, st);
+    }
+}
+
+}  // namespace gsr

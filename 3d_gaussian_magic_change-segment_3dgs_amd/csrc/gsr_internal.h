@@ -4,6 +4,7 @@
 #include <stdint.h>
 #include <stddef.h>
 
+#include <algorithm>
 #include <string>
 
 #include "../../include/gsr.h"
@@ -89,6 +90,10 @@ inline SortWs sort_ws(size_t n, void* p) {
             c + hdr + align_up(nt * RADIX * 4)};
 }
 
+// binning_rows.hip workspace sizes (used by the layouts below)
+size_t rows_bin_geom_ws_bytes(size_t P, int gy);
+size_t rows_bin_ws_bytes(size_t cap);
+
 // ---- geometry buffer (reference GeometryState, rasterizer_impl.cu:155-171) ----
 struct GeomLayout {
     size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, goff, ws,
@@ -108,7 +113,8 @@ inline GeomLayout geom_layout(size_t P) {
     L.dkeys_alt = take(P * 4);
     L.offsets = take(P * 4);
     L.goff = take(P * 4);
-    L.ws = take(sort_ws_bytes(P, MAX_SORT_PASSES));  // depth sort
+    // depth sort; afterwards the row binning's level-1 table (binning_rows.hip)
+    L.ws = take(std::max(sort_ws_bytes(P, MAX_SORT_PASSES), rows_bin_geom_ws_bytes(P, 255)));
     L.ws_scan = take(scan_ws_bytes(P));              // tiles_touched scan
     // tile rect packed as x0 | y0 << 8 | x1 << 16 | y1 << 24 (grids up to 255 x 255 tiles):
     // the depth sort carries it, so the scan and the duplicate read it in depth order
@@ -139,7 +145,7 @@ inline BinLayout bin_layout(size_t I) {
     L.gid_alt = take(I * 4);
     L.point_list = take(I * 4);
     L.written = take(cdiv(I, 16) * 16);  // backward: 1 byte per instance slot (zeroed by the tile sort's last pass)
-    L.ws = take(sort_ws_bytes(I, MAX_SORT_PASSES));
+    L.ws = take(std::max(sort_ws_bytes(I, MAX_SORT_PASSES), rows_bin_ws_bytes(I)));  // tile sort or row binning
     L.bytes = o + ALIGN;
     return L;
 }
@@ -240,6 +246,18 @@ void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st);
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
                                   void* ws, bool ws_zeroed, hipStream_t st, uint32_t* host_total = nullptr,
                                   bool rect_mode = false);
+// exclusive scan of n (or min(n, *n_dev)) values; W zeroed beforehand
+void launch_scan_exclusive(const uint32_t* src, uint32_t* out, size_t n, const uint32_t* n_dev, const ScanWs& W,
+                           hipStream_t st);
+// binning_rows.hip: tile lists by row-then-tile expansion (grids up to 255 x 255 tiles).
+// stage 0: level 1 (rows, goff); 1: level 2 (point_list, slot_vals, written flags
+// cleared); 2: ranges + heavy-first tile order.  geom_ws: rows_bin_geom_ws_bytes(P, gy)
+// bytes (the depth sort's workspace, free by then); bin_ws: rows_bin_ws_bytes(cap).
+void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uint32_t* offsets, const uint32_t* rect,
+                         uint32_t* goff, void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_u, uint32_t* e_x,
+                         uint32_t* point_list, uint32_t* slot_vals, uint2* ranges, uint32_t* tile_order,
+                         uint4* written, size_t written16, size_t cap, const uint32_t* n_total, hipStream_t st,
+                         int stage);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, const uint32_t* rect_sorted, int gx, uint32_t* tkeys,
                       uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, uint32_t cap, hipStream_t st);
