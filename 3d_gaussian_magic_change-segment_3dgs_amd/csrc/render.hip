@@ -478,7 +478,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     // Same two-stage batch pipeline and LDS record broadcast as the forward, walking
     // the list back to front: lane l of the batch with upper end `top` owns position top-1-l.
     __shared__ float4 srec[64][4];
-    const int top0 = (int)maxlast;
+    const int top0 = (int)__builtin_amdgcn_readfirstlane(maxlast);
     const uint32_t* plist = point_list + range.x;
     const uint32_t* slist = slot_vals + range.x;
     // list positions below 0 are clamped to 0 (unconditional loads, see fetch_batch)
@@ -512,6 +512,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
             const float pmin = power_floor(rb.y);
             const bool hit = lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1);
             uint64_t todo = __ballot(hit);
+            // Lanes replaying every position of this batch (p < n_contrib for all p < top) and
+            // whether any lane starts replaying inside it: only then is p < n_contrib
+            // tested per instance.
+            uint64_t act_all[4];
+            bool varying = false;
+    #pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                act_all[k] = __builtin_amdgcn_ballot_w64(lastc[k] >= (uint32_t)top);
+                varying |= lastc[k] < (uint32_t)top && lastc[k] > (uint32_t)(top - cnt);
+            }
+            const bool vary = wave_any(varying);
+            STAT(9, vary);
             STAT(2, cnt - __popcll(todo));
             __syncthreads();  // previous batch's reads are done
             srec[lane][0] = ra;                                                   // x, y, conic a, b
@@ -526,6 +538,11 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                 const float4 q0 = srec[j][0], q1 = srec[j][1];
                 const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
                 float power[4], dys[4];
+                uint64_t act[4] = {act_all[0], act_all[1], act_all[2], act_all[3]};
+                if (vary) {
+    #pragma unroll
+                    for (int k = 0; k < 4; ++k) act[k] = __builtin_amdgcn_ballot_w64(p < lastc[k]);
+                }
                 uint64_t near[4];  // per strip: lanes whose pixel replays p and is within reach
                 const float dx = gx_ - pfx;
                 const float adxdx = ca * dx * dx, bdx = cb * dx;
@@ -534,7 +551,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                     const float dy = gy_ - pfy[k];
                     dys[k] = dy;
                     power[k] = __builtin_fmaf(-0.5f, adxdx + cc * dy * dy, -(bdx * dy));  // == -0.5 S - B
-                    near[k] = __builtin_amdgcn_ballot_w64(p < lastc[k]) & __builtin_amdgcn_ballot_w64(power[k] >= pm);
+                    near[k] = act[k] & __builtin_amdgcn_ballot_w64(power[k] >= pm);
                 }
                 STAT(0, 1);
                 if (!(near[0] | near[1] | near[2] | near[3])) {
@@ -542,7 +559,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                     continue;
                 }
                 STAT(3, 1);
-                const float4 q2 = srec[j][2], q3 = srec[j][3];
+                                const float4 q2 = srec[j][2], q3 = srec[j][3];
                 const float op = q1.z, dep = q3.x, s0 = q1.w;
                 const float c0 = q2.x, c1 = q2.y, c2 = q2.z, s1 = q2.w;
                 const uint32_t u = __float_as_uint(q3.y);

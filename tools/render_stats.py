@@ -37,8 +37,7 @@ def main():
         print(f"{name}: instances={inst} batches={batches} prefiltered={pre} zero_tail={tail} visited={it} "
               f"near_skip={ns} ({ns / max(it, 1):.1%}) full={full} strips={strips} ({strips / max(full, 1):.2f}/full) "
               f"ok_px={okpx} lane_eff={okpx / max(64 * strips, 1):.1%}")
-    print(f"fwd geometric reach per visited pair: 16x4 strips {s[9] / max(s[0], 1):.3f}, "
-          f"8x8 blocks {s[10] / max(s[0], 1):.3f}")
+    print(f"bwd batches with a lane whose replay starts inside the batch: {s[16 + 9]} of {s[16 + 5]}")
 
 
 if __name__ == "__main__":
