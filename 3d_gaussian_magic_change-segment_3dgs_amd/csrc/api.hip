@@ -181,6 +181,40 @@ namespace gsr {
 int set_error(const std::string& msg) { return fail(msg); }
 }  // namespace gsr
 
+
+namespace gsr {
+namespace {
+// HBM streaming-copy reference for the roofline (bench.py): each thread moves U float4s,
+// all loads issued before the stores, non-temporal on both sides.
+template <int U>
+__global__ void __launch_bounds__(256) k_stream_copy(const float4* __restrict__ src, float4* __restrict__ dst,
+                                                     size_t n) {
+    const size_t base = ((size_t)blockIdx.x * 256 * U) + threadIdx.x;
+    float4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * 256;
+        if (i < n) {
+            const float* s = (const float*)(src + i);
+            v[u] = make_float4(__builtin_nontemporal_load(s), __builtin_nontemporal_load(s + 1),
+                               __builtin_nontemporal_load(s + 2), __builtin_nontemporal_load(s + 3));
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const size_t i = base + (size_t)u * 256;
+        if (i < n) {
+            float* d = (float*)(dst + i);
+            __builtin_nontemporal_store(v[u].x, d);
+            __builtin_nontemporal_store(v[u].y, d + 1);
+            __builtin_nontemporal_store(v[u].z, d + 2);
+            __builtin_nontemporal_store(v[u].w, d + 3);
+        }
+    }
+}
+}  // namespace
+}  // namespace gsr
+
 extern "C" {
 
 const char* gsr_last_error(void) { return g_last_error.c_str(); }
@@ -688,6 +722,25 @@ int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const
     hipStream_t st = (hipStream_t)stream;
     gsr::launch_mark_visible(P, means3D, viewmatrix, present, st);
     if (int rc = check("mark_visible", st, false)) return rc;
+    return 0;
+}
+
+
+int gsr_stream_copy(const void* src, void* dst, size_t bytes, int per_thread, void* stream) {
+    g_last_error.clear();
+    if (!src || !dst || bytes % 16) return fail("[gsr] stream_copy: null buffer or size not a multiple of 16");
+    const size_t n = bytes / 16;
+    if (n == 0) return 0;
+    hipStream_t st = (hipStream_t)stream;
+    const auto* s4 = (const float4*)src;
+    auto* d4 = (float4*)dst;
+    switch (per_thread) {
+        case 1: hipLaunchKernelGGL(gsr::k_stream_copy<1>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, s4, d4, n); break;
+        case 2: hipLaunchKernelGGL(gsr::k_stream_copy<2>, dim3((unsigned)((n + 511) / 512)), dim3(256), 0, st, s4, d4, n); break;
+        case 4: hipLaunchKernelGGL(gsr::k_stream_copy<4>, dim3((unsigned)((n + 1023) / 1024)), dim3(256), 0, st, s4, d4, n); break;
+        default: return fail("[gsr] stream_copy: per_thread must be 1, 2 or 4");
+    }
+    if (int rc = check("stream_copy", st, false)) return rc;
     return 0;
 }
 

@@ -114,10 +114,13 @@ _lib.gsr_stage_name.argtypes = [_i]
 _lib.gsr_timing_enable.argtypes = [_i]
 _lib.gsr_timing_collect.restype = _i
 _lib.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_longlong)]
+_lib.gsr_stream_copy.restype = _i
+_lib.gsr_stream_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, _i, ctypes.c_void_p]
 
 EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_binning_capacity", "gsr_img_bytes", "gsr_backward_scratch_bytes",
                     "gsr_forward_geometry", "gsr_forward_render", "gsr_forward", "gsr_backward", "gsr_mark_visible",
                     "gsr_debug_copy", "gsr_num_stages", "gsr_stage_name", "gsr_timing_enable", "gsr_timing_collect",
+                    "gsr_stream_copy",
                     "gsr_last_error", "gsr_version", "gsr_set_option", "gsr_multiview_scratch_bytes",
                     "gsr_backward_multiview", "gsr_sh_rows_floats", "gsr_backward_multiview_deferred_sh",
                     "gsr_sh_backward")

@@ -17,10 +17,11 @@ backward and one exchange per step (--views-per-gpu sets the main mode).
 Prints ONE JSON line on rank 0.  Extra objects:
   roofline     -- the dominant kernel (per-stage HIP events recorded by libgsr on
                   the stream it launches on): algorithmic bytes per launch / mean
-                  launch time vs the 8 TB/s HBM peak; `traffic` = PMC-measured HBM
+                  launch time vs the 8 TB/s HBM peak and vs the streaming-copy rate
+                  measured on the box (gsr_stream_copy); `traffic` = PMC-measured HBM
                   bytes per launch from profiles/ when a counter profile exists;
-                  `valu_issue_frac` = PMC SQ_INSTS_VALU x 4 cycles / (1024 SIMDs x
-                  2.4 GHz x launch time): the bound the render kernels actually hit.
+                  `cycles_per_valu_instr` = SIMD cycles per PMC VALU instruction (the
+                  render kernels are bound by VALU issue and latency, not bytes).
   train_step   -- (N = 1) the s8f training step around the rasterizer: fused Adam
                   step / activation backward kernels vs the reference's torch
                   optimizer + activations on the same GPU (gsr_tools/train_bench.py).
@@ -47,7 +48,9 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 SIMD_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "round1_pmc_summary.json")
+# newest committed counter summary (tools/pmc.sh + tools/pmc_summary.py)
+PMC_SUMMARY = next((os.path.join(ROOT, "profiles", f) for f in ("round2_pmc_summary.json", "round1_pmc_summary.json")
+                    if os.path.exists(os.path.join(ROOT, "profiles", f))), "")
 
 
 EXCHANGE_DESC = {
@@ -89,24 +92,74 @@ def view_bytes(P, I, HW, deg):
     return (446 + 36 * M) * P + 148 * I + 68 * HW
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def cpu_baseline(scene, cam, grads, budget_s=20.0):
+    """The CPU oracle on whole views of the benchmark workload (fwd and bwd timed apart),
+    plus BASELINE config C1 (10k Gaussians, SH0, 256x256) for scale."""
     from oracle import oracle as O
+    from gsr_tools.scene import config_scene_and_camera
     O.build()
     up = [grads[k].numpy() for k in ("color", "segment", "depth", "alpha")]
-    t0 = time.perf_counter()
-    r = O.run_scene(scene, cam)
-    r.backward(*up)
-    one = time.perf_counter() - t0
+
+    def views(sc, cm, ups, reps):
+        tf = tb = 0.0
+        for _ in range(reps):
+            t0 = time.perf_counter()
+            r = O.run_scene(sc, cm)
+            t1 = time.perf_counter()
+            r.backward(*ups)
+            tb += time.perf_counter() - t1
+            tf += t1 - t0
+        return tf, tb
+
+    one = sum(views(scene, cam, up, 1))  # warm-up view
     reps = int(max(1, min(10, budget_s // max(one, 1e-3))))
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        r = O.run_scene(scene, cam)
-        r.backward(*up)
-    el = time.perf_counter() - t0
-    return {"value": reps / el, "unit": "views/s", "cores": int(O.lib().oracle_num_threads()), "kind": "port",
+    tf, tb = views(scene, cam, up, reps)
+    s1, c1 = config_scene_and_camera("c1")
+    g1 = torch.Generator().manual_seed(1)
+    up1 = [(torch.randn(c, c1.height, c1.width, generator=g1) * 1e-3).numpy() for c in (3, 2, 1, 1)]
+    views(s1, c1, up1, 1)
+    r1 = 20
+    tf1, tb1 = views(s1, c1, up1, r1)
+    return {"value": round(reps / (tf + tb), 4), "unit": "views/s", "cores": int(O.lib().oracle_num_threads()),
+            "kind": "port", "cpu_model": cpu_model(),
+            "fwd_ms_per_view": round(1e3 * tf / reps, 1), "bwd_ms_per_view": round(1e3 * tb / reps, 1),
+            "c1": {"value": round(r1 / (tf1 + tb1), 2), "unit": "views/s", "fwd_ms_per_view": round(1e3 * tf1 / r1, 2),
+                   "bwd_ms_per_view": round(1e3 * tb1 / r1, 2),
+                   "sample": f"{r1} views of C1 (P={s1.P}, {c1.width}x{c1.height}, SH{s1.sh_degree})"},
             "sample": f"{reps} whole fwd+bwd views of the benchmark workload (P={scene.P}, "
                       f"{cam.width}x{cam.height}, SH{scene.sh_degree}) after 1 warm-up view; "
                       f"oracle/gsr_oracle.cpp built -O3 -fopenmp"}
+
+
+def stream_copy_peak(lib, device, nbytes=1 << 30):
+    """Achievable HBM rate on this box: gsr_stream_copy (float4, non-temporal loads and
+    stores) of `nbytes`, best of 1/2/4 float4 per thread, read + write bytes / time."""
+    src = torch.empty(nbytes // 4, dtype=torch.float32, device=device).fill_(1.0)
+    dst = torch.empty_like(src)
+    st = torch.cuda.current_stream(device).cuda_stream
+    best = 0.0
+    for u in (1, 2, 4):
+        lib.gsr_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, u, st)
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(10):
+            lib.gsr_stream_copy(src.data_ptr(), dst.data_ptr(), nbytes, u, st)
+        b.record()
+        b.synchronize()
+        best = max(best, 2 * nbytes * 10 / (a.elapsed_time(b) * 1e-3) / 1e9)
+    del src, dst
+    torch.cuda.empty_cache()
+    return round(best, 1)
 
 
 def main():
@@ -238,25 +291,33 @@ def main():
 
     step = make_step(B)
 
-    def timed(fn, k):
+    def timed(fn, k, per_step=None):
         """k steps between a barrier + device sync on both sides; max over ranks.  Python's
         cyclic GC is paused inside (collected just before): a collection pass in the
         middle of the loop stalls the host for milliseconds, which leaves the GPU idle
-        behind the per-view num_rendered sync."""
+        behind the per-view num_rendered sync.  per_step (a list) receives each step's
+        duration from events recorded on the compute stream between the steps."""
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(k + 1)] if per_step is not None else None
         gc.collect()
         gc.disable()
         if dist is not None:
             dist.barrier()
         torch.cuda.synchronize()
         t_start = time.perf_counter()
-        for _ in range(k):
+        if evs:
+            evs[0].record()
+        for i in range(k):
             fn()
+            if evs:
+                evs[i + 1].record()
         drain()
         torch.cuda.synchronize()
         gc.enable()
         if dist is not None:
             dist.barrier()
         el = time.perf_counter() - t_start
+        if evs:
+            per_step.extend(evs[i].elapsed_time(evs[i + 1]) for i in range(k))
         if dist is not None:
             t = torch.tensor([el], device=device, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -291,7 +352,8 @@ def main():
     sms, scnt = collect()
     dom_i = max(range(nst), key=lambda i: sms[i]) if any(scnt) else 0
     _C._lib.gsr_timing_enable(1 << dom_i)
-    elapsed = timed(step, args.steps)
+    step_ms = []
+    elapsed = timed(step, args.steps, step_ms)
     _C._lib.gsr_timing_enable(0)
     ms, cnt = collect()  # the dominant stage's launches inside the timed region
     I, HW = int(state["I"]), W * H
@@ -309,26 +371,38 @@ def main():
     if dom and cnt[dom_i]:
         avg_live = ms[dom_i] / cnt[dom_i]  # measured inside the timed region
         achieved = round(algorithmic_bytes(dom, P, I, HW, deg, B) / (avg_live * 1e-3) / 1e9, 1)
-        traffic = valu_frac = None
-        if os.path.exists(PMC_SUMMARY):
+        traffic = cyc_per_valu = None
+        if PMC_SUMMARY:
             try:
                 pk = json.load(open(PMC_SUMMARY)).get("kernels", {}).get(dom, {})
                 traffic = pk.get("hbm_bytes_per_launch")
                 if pk.get("SQ_INSTS_VALU"):
-                    # wave64 VALU issue = 4 cycles on one of 1024 SIMDs, at the 2.4 GHz peak clock
-                    valu_frac = round(pk["SQ_INSTS_VALU"] * 4 / 1024 / (SIMD_CLOCK_HZ * avg_live * 1e-3), 4)
+                    # SIMD cycles per wave64 VALU instruction at the 2.4 GHz peak clock over the
+                    # 1024 SIMDs: ~2.6-3.0 is the issue floor of plain f32 ops, 4.2-4.6 of compares,
+                    # selects, min/max, shifts and SGPR-operand ops, ~8.5 of v_exp/v_rcp
+                    # (tools/valu_mix_probe.hip, profiles/round2_valu_mix_probe.txt)
+                    cyc_per_valu = round(SIMD_CLOCK_HZ * avg_live * 1e-3 * 1024 / pk["SQ_INSTS_VALU"], 3)
             except Exception:
-                traffic = valu_frac = None
+                traffic = cyc_per_valu = None
+        measured_peak = stream_copy_peak(_C._lib, device) if rank == 0 else None
         roof = {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "measured_copy_peak": measured_peak,
+                "frac_of_measured_peak": round(achieved / measured_peak, 4) if measured_peak else None,
                 "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg, B),
                 "avg_launch_ms": round(avg_live, 4), "launches_timed": int(cnt[dom_i]),
-                "valu_issue_frac": valu_frac,
+                "valu_instr_per_launch": (json.load(open(PMC_SUMMARY)).get("kernels", {}).get(dom, {}).get("SQ_INSTS_VALU")
+                                          if PMC_SUMMARY else None),
+                "cycles_per_valu_instr": cyc_per_valu,
                 "whole_view_frac": round(view_bytes(P, I, HW, deg) * value / world / 1e9 / HBM_PEAK_GBS, 4)}
     out = {
         "metric": "forward+backward views/sec @1080p, 1M Gaussians, 1/2/4/8 MI355X",
         "value": round(value, 2), "unit": "views/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 4), "higher_is_better": True, "scaling": "weak",
+        "step_ms": ({"mean": round(sum(step_ms) / len(step_ms), 4),
+                     "median": round(sorted(step_ms)[len(step_ms) // 2], 4),
+                     "p90": round(sorted(step_ms)[min(len(step_ms) - 1, int(0.9 * len(step_ms)))], 4),
+                     "source": "hipEvents between steps on the compute stream (rank 0)"} if step_ms else None),
         "vs_baseline": None, "dtype": "f32", "data": "synthetic (SURVEY.md s8d generator, seed 0; upstream grads "
                                                     "N(0,1)*1e-3 seed 1)",
         "config": {"workload": f"{args.config}: P={P} Gaussians, SH{deg}, {W}x{H}, fwd+bwd per view; {B} view(s) per "
@@ -350,7 +424,7 @@ def main():
         for _ in range(max(1, args.warmup // 4)):
             bstep()
         drain()
-        k = max(2, args.steps // BB)
+        k = max(8, args.steps // BB)
         el_b = timed(bstep, k)
         out["batched"] = {"views_per_step_per_gpu": BB, "global_batch": world * BB, "steps": k,
                           "value": round(world * BB * k / el_b, 2), "unit": "views/s",

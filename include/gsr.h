@@ -251,6 +251,12 @@ GSR_API const char* gsr_stage_name(int stage);
 GSR_API void gsr_timing_enable(int stage_mask);
 GSR_API int gsr_timing_collect(double* ms, long long* counts);
 
+/* HBM streaming-copy reference for the roofline (not part of the reference's interface):
+ * copies `bytes` (a multiple of 16) from src to dst with `per_thread` (1, 2 or 4) float4 per
+ * thread, non-temporal loads and stores, on `stream`.  bench.py times it with events to
+ * report the achievable HBM rate of the box beside the 8 TB/s spec. */
+GSR_API int gsr_stream_copy(const void* src, void* dst, size_t bytes, int per_thread, void* stream);
+
 /* Thread-local message of the last failing call ("" if none). */
 GSR_API const char* gsr_last_error(void);
 

@@ -1,0 +1,20 @@
+#!/bin/bash
+# round_profile.sh TAG: the round's evidence in one GPU session -> gpurun_out/TAG/
+#   pytest -m gpu, the default bench line (CPU baseline, train step), rocprofv3 kernel
+#   stats of a 30-step bench, and the PMC passes (tools/pmc.sh) summarised.
+# Stops at the first failing step.
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+TAG=${1:-latest}
+O=gpurun_out/$TAG
+rm -rf $O; mkdir -p $O
+timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
+tail -2 $O/pytest_gpu.log
+timeout -k 10 400 python bench.py --stages > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+cat $O/bench.json; grep -v amdgpu.ids $O/bench.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o kt --output-format csv -- python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-train --batched-views 1 > $O/prof_bench.log 2>&1 || { tail -20 $O/prof_bench.log; exit 1; }
+cp $(find $O/prof -name "*kernel_stats.csv" | head -1) $O/kernel_stats.csv
+python tools/kstats.py $O/kernel_stats.csv
+bash tools/pmc.sh > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
+python tools/pmc_summary.py $O/pmc_summary.json | grep -E "^render|^gaussian|^preprocess"
