@@ -293,12 +293,22 @@ struct Cam {
     f3 campos;
 };
 
-// Camera matrices live in device memory (the reference passes CUDA tensors);
-// one uniform load per wave through the scalar cache.
+// Camera matrices live in device memory (the reference passes CUDA tensors); they are
+// read through the constant address space, i.e. as scalar (SMEM) loads into SGPRs: the
+// compiler cannot prove on its own that no store of the kernel aliases them, and plain
+// loads become per-lane vector loads issued late behind the kernel's other memory work.
+// (The forward preprocess keeps plain loads: measured faster there, 0.0695 vs 0.0736 ms.)
 __device__ __forceinline__ void load_cam(const gsr_settings& s, Cam& c) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) { c.view[i] = s.viewmatrix[i]; c.proj[i] = s.projmatrix[i]; }
     c.campos = ld3(s.campos);
+}
+typedef const __attribute__((address_space(4))) float* const_fp;
+__device__ __forceinline__ void load_cam_smem(const gsr_settings& s, Cam& c) {
+    const const_fp V = (const_fp)s.viewmatrix, Pm = (const_fp)s.projmatrix, C = (const_fp)s.campos;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) { c.view[i] = V[i]; c.proj[i] = Pm[i]; }
+    c.campos = {C[0], C[1], C[2]};
 }
 
 // ------------------------------------------------------------------ forward --
@@ -491,15 +501,28 @@ __device__ __forceinline__ void sum_records(const float* __restrict__ contrib, c
     double d[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) d[j] = 0.0;
-    // Written flags (one byte per slot, 0 or 1) are read 8 at a time and folded into an
-    // 8-bit mask (byte i -> bit i); then four records per round, their loads issued
+    // Written flags (one byte per slot, 0 or 1) are read 32 at a time -- four 8-byte words
+    // whose loads are issued together -- and folded into a 32-bit mask (slot i -> bit i);
+    // then the written records of those 32 slots, four per round with their loads issued
     // together (clamped slot indices: a record-at-a-time loop leaves one load in flight
-    // per lane).  Sums stay in slot order.
+    // per lane).  A Gaussian covering many tiles thus costs one flag round trip per 32
+    // slots instead of one per 8 (the gather was 66 of the kernel's 143 us, most of it in
+    // the long ranges' serial round trips).  Sums stay in slot order.
     const uint64_t* w8 = reinterpret_cast<const uint64_t*>(written);
-    for (uint32_t w = lo >> 3; w <= (hi - 1) >> 3; ++w) {
-        uint32_t bits = (uint32_t)(((w8[w] & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
-        if (w == lo >> 3) bits &= 0xFFu << (lo & 7);
-        if (w == (hi - 1) >> 3 && ((hi & 7) != 0)) bits &= ~(0xFFu << (hi & 7));
+    const uint32_t wlo = lo >> 3, whi = (hi - 1) >> 3;
+    for (uint32_t w = wlo; w <= whi; w += 4) {
+        uint64_t f[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) f[k] = w8[min(w + (uint32_t)k, whi)];
+        uint32_t bits = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            uint32_t b = (uint32_t)(((f[k] & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+            if (w + k == wlo) b &= 0xFFu << (lo & 7);
+            if (w + k == whi && ((hi & 7) != 0)) b &= ~(0xFFu << (hi & 7));
+            if (w + k > whi) b = 0;
+            bits |= b << (8 * k);
+        }
         while (bits) {
             uint32_t u[4];
             bool v[4];
@@ -554,7 +577,36 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
     const int M = s.M;
     const size_t i3 = 3 * (size_t)idx;
     const bool live = idx < s.P;
-    const bool vis = live && radii[idx] > 0;
+    // Every per-Gaussian input that does not depend on the record sums is loaded up front
+    // (clamped index for the tail threads), so that their latencies overlap each other
+    // and the record gather instead of forming a chain of round trips after it.
+    const int ci = live ? idx : 0;
+    const size_t c3i = 3 * (size_t)ci;
+    Cam cam;
+    load_cam_smem(s, cam);
+    const int rad = radii[ci];
+    const uint32_t lo_slot = goff[ci], n_slot = tiles_touched[ci];
+    const float4 r0 = rec[(size_t)ci * REC_F4], r1 = rec[(size_t)ci * REC_F4 + 1];
+    const f3 mean = ld3(in.means3D + c3i);
+    float c3[6];
+    float4 quat = make_float4(0.f, 0.f, 0.f, 0.f);
+    f3 scale = {0.f, 0.f, 0.f};
+    if (in.cov3D_precomp) {
+#pragma unroll
+        for (int i = 0; i < 6; ++i) c3[i] = in.cov3D_precomp[6 * (size_t)ci + i];
+    } else {
+        quat = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)ci);
+        scale = ld3(in.scales + c3i);
+    }
+    const uint8_t cbits = in.shs ? clamped[ci] : 0;
+    f3 jx = {0, 0, 0}, jy = {0, 0, 0}, jz = {0, 0, 0};
+    if (in.shs && s.D > 0) {
+        const float* J = jac_row(shjac, ci);
+        jx = {J[0], J[64], J[128]};
+        jy = {J[192], J[256], J[320]};
+        jz = {J[384], J[448], J[512]};
+    }
+    const bool vis = live && rad > 0;
     // dsh rows (48 floats = 192 B per Gaussian) are written through LDS so that the
     // stores are contiguous runs of the wave's 12 KB output block: a thread storing
     // its own row issues 16-B stores 192 B apart, which measured at 0.09 ms of the
@@ -579,9 +631,8 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
     if (vis) {
         // gather-sum of the written instance records of the Gaussian's slot range
         // [goff, goff + tiles_touched), in slot order (deterministic).
-        const float4 r0 = rec[(size_t)idx * REC_F4], r1 = rec[(size_t)idx * REC_F4 + 1];
         float q[12];
-        sum_records(contrib, written, goff[idx], goff[idx] + tiles_touched[idx], q);
+        sum_records(contrib, written, lo_slot, lo_slot + n_slot, q);
         const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
         const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * s.W);
         const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * s.H);
@@ -590,24 +641,11 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         if (g.dopacity) g.dopacity[idx] = q[6];
         if (g.dsegments) { g.dsegments[2 * (size_t)idx] = q[3]; g.dsegments[2 * (size_t)idx + 1] = q[4]; }
 
-        Cam cam;
-        load_cam(s, cam);
         const float focal_y = s.H / (2.0f * s.tanfovy);
         const float focal_x = s.W / (2.0f * s.tanfovx);
-        const f3 mean = ld3(in.means3D + i3);
 
         // ---- computeCov2DCUDA (backward.cu:155-273)
-        float c3[6];
-        float4 quat = make_float4(0.f, 0.f, 0.f, 0.f);
-        f3 scale = {0.f, 0.f, 0.f};
-        if (in.cov3D_precomp) {
-#pragma unroll
-            for (int i = 0; i < 6; ++i) c3[i] = in.cov3D_precomp[6 * (size_t)idx + i];
-        } else {
-            quat = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)idx);
-            scale = ld3(in.scales + i3);
-            cov3d_from(scale, s.scale_modifier, quat, c3);  // == the forward's geom.cov3D
-        }
+        if (!in.cov3D_precomp) cov3d_from(scale, s.scale_modifier, quat, c3);  // == the forward's geom.cov3D
         const float dcx = -0.5f * op * q[9], dcy = -0.5f * op * q[10], dcz = -0.5f * op * q[11];
         const EwaTerms e = ewa_terms(mean, focal_x, focal_y, s.tanfovx, s.tanfovy, cam.view);
         const float x_grad_mul = e.txtz < -e.limx || e.txtz > e.limx ? 0 : 1;
@@ -695,18 +733,12 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
             const int deg = s.D;
             const f3 dir_orig = m - cam.campos;
             const f3 dir = dir_orig / sqrtf(dot3(dir_orig, dir_orig));
-            const uint8_t cb = clamped[idx];
+            const uint8_t cb = cbits;
             f3 dRGB = {q[0], q[1], q[2]};
             dRGB.x *= (cb & 1) ? 0 : 1;
             dRGB.y *= (cb & 2) ? 0 : 1;
             dRGB.z *= (cb & 4) ? 0 : 1;
-            f3 dx = {0, 0, 0}, dy = {0, 0, 0}, dz = {0, 0, 0};
-            if (deg > 0) {
-                const float* J = jac_row(shjac, idx);
-                dx = {J[0], J[64], J[128]};
-                dy = {J[192], J[256], J[320]};
-                dz = {J[384], J[448], J[512]};
-            }
+            const f3 dx = jx, dy = jy, dz = jz;
             // dL/dsh[i] = basis_i * dRGB (backward.cu:46-110); coefficients >= (D+1)^2 get 0
             sh_basis(deg, dir, bas);
             dc[0] = dRGB.x;
