@@ -38,6 +38,10 @@ namespace {
 
 constexpr int RB_CH = 512;            // items per chunk = threads per block
 constexpr int RB_W = RB_CH / 32;      // bitmask words per bucket
+// LDS words per bucket row of bits / pre: one pad word so that the words of different
+// buckets fall in different banks (with a stride of 16 words, lanes touching buckets 4
+// apart hit one bank: 13M bank-conflict cycles per tile-scatter launch at the metric scene)
+constexpr int RB_S = RB_W + 1;
 constexpr int RB_STAGE = 2048;        // outputs a chunk assembles in LDS (more: direct writes)
 constexpr int RB_MAXB = 256;          // buckets per chunk (<= 255 rows / columns)
 constexpr int RB_GRID2 = 2048;        // blocks of the level-2 kernels (grid-stride over chunks)
@@ -72,14 +76,14 @@ __device__ void lds_scan256(const uint32_t* v, int n, uint32_t* out, uint32_t* t
     __syncthreads();
 }
 
-// bits[b * RB_W + w]: bit i of word w = item 32 w + i of the chunk covers bucket b.
-// pre[b * RB_W + w] = items of bucket b in words < w; cnt[b] = items of bucket b.
+// bits[b * RB_S + w]: bit i of word w = item 32 w + i of the chunk covers bucket b.
+// pre[b * RB_S + w] = items of bucket b in words < w; cnt[b] = items of bucket b.
 __device__ void bucket_prefix(const uint32_t* bits, int nb, uint32_t* pre, uint32_t* cnt) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     constexpr int PER_WAVE = 64 / RB_W;  // buckets per wave pass
     for (int b0 = PER_WAVE * wave; b0 < nb; b0 += PER_WAVE * (RB_CH / 64)) {
         const int b = b0 + lane / RB_W, w = lane % RB_W;
-        const uint32_t c = b < nb ? (uint32_t)__popc(bits[b * RB_W + w]) : 0u;
+        const uint32_t c = b < nb ? (uint32_t)__popc(bits[b * RB_S + w]) : 0u;
         uint32_t x = c;
 #pragma unroll
         for (int o = 1; o < RB_W; o <<= 1) {
@@ -87,7 +91,7 @@ __device__ void bucket_prefix(const uint32_t* bits, int nb, uint32_t* pre, uint3
             if (w >= o) x += y;
         }
         if (b < nb) {
-            pre[b * RB_W + w] = x - c;
+            pre[b * RB_S + w] = x - c;
             if (w == RB_W - 1) cnt[b] = x;
         }
     }
@@ -127,7 +131,7 @@ __global__ void __launch_bounds__(RB_CH) k_rows_count(int P, int gy, int nch1, c
 
 // Level-1 entries (E1, grouped by row): e_gid = Gaussian id, e_u = its first instance slot
 // in the row, e_x = x0 | x1 << 8.  Also goff[gid] (the backward's record slots).
-// Dynamic LDS: bits + pre, 2 x gy x RB_W words (sized by the grid, not the 255 bound:
+// Dynamic LDS: bits + pre, 2 x gy x RB_S words (sized by the grid, not the 255 bound:
 // four blocks per CU at 1080p).  Every global load is issued before the first barrier.
 __global__ void __launch_bounds__(RB_CH) k_rows_scatter(int P, int gy, int nch1, const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ offsets,
@@ -137,7 +141,7 @@ __global__ void __launch_bounds__(RB_CH) k_rows_scatter(int P, int gy, int nch1,
                                                         uint32_t* __restrict__ e_x, uint32_t cap) {
     extern __shared__ uint32_t dyn[];
     uint32_t* bits = dyn;
-    uint32_t* pre = dyn + gy * RB_W;
+    uint32_t* pre = dyn + gy * RB_S;
     __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
     __shared__ uint32_t s_gid[RB_STAGE], s_u[RB_STAGE], s_x[RB_STAGE];
     __shared__ uint32_t tot;
@@ -150,13 +154,13 @@ __global__ void __launch_bounds__(RB_CH) k_rows_scatter(int P, int gy, int nch1,
         g = order[r];
         off = r == 0 ? 0u : offsets[r - 1];
     }
-    for (int i = tid; i < gy * RB_W; i += RB_CH) bits[i] = 0;
+    for (int i = tid; i < gy * RB_S; i += RB_CH) bits[i] = 0;
     for (int y = tid; y < gy; y += RB_CH) gb[y] = base1[(size_t)y * nch1 + blockIdx.x];
     __syncthreads();
     const bool vis = x1 > x0 && y1 > y0;
     const uint32_t bit = 1u << (tid & 31), wd = (uint32_t)tid >> 5;
     if (vis)
-        for (int y = y0; y < y1; ++y) atomicOr(&bits[y * RB_W + wd], bit);
+        for (int y = y0; y < y1; ++y) atomicOr(&bits[y * RB_S + wd], bit);
     __syncthreads();
     bucket_prefix(bits, gy, pre, cnt);
     lds_scan256(cnt, gy, lst, &tot);
@@ -165,7 +169,7 @@ __global__ void __launch_bounds__(RB_CH) k_rows_scatter(int P, int gy, int nch1,
         goff[g] = off;
         const uint32_t w = (uint32_t)(x1 - x0), below = bit - 1u;
         for (int y = y0; y < y1; ++y) {
-            const uint32_t rank = pre[y * RB_W + wd] + (uint32_t)__popc(bits[y * RB_W + wd] & below);
+            const uint32_t rank = pre[y * RB_S + wd] + (uint32_t)__popc(bits[y * RB_S + wd] & below);
             const uint32_t u = off + (uint32_t)(y - y0) * w;
             const uint32_t xr = (uint32_t)x0 | ((uint32_t)x1 << 8) | ((uint32_t)y << 16);
             if (staged) {
@@ -269,7 +273,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_count(int gx, int gy, int nch1,
 // tiles {0, 0}); also clears the backward's written-slot flags.  The next chunk's entries
 // and bucket bases are loaded while the current one is ranked (software pipeline: a chunk
 // otherwise waits on two dependent global round trips).  Dynamic LDS: bits + pre,
-// 2 x gx x RB_W words.
+// 2 x gx x RB_S words.
 __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch1, const uint32_t* __restrict__ table1,
                                                          const uint32_t* __restrict__ base1,
                                                          const uint32_t* __restrict__ base2,
@@ -282,7 +286,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
                                                          uint2* __restrict__ ranges, uint4* zero, size_t nzero16) {
     extern __shared__ uint32_t dyn[];
     uint32_t* bits = dyn;
-    uint32_t* pre = dyn + gx * RB_W;
+    uint32_t* pre = dyn + gx * RB_S;
     __shared__ RowMap m;
     __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
     __shared__ uint32_t s_gid[RB_STAGE], s_u[RB_STAGE];
@@ -319,13 +323,13 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
     if (c < m.nch2) cur = fetch(c);
     while (c < m.nch2) {
         const int y = cur.y;
-        for (int i = tid; i < gx * RB_W; i += RB_CH) bits[i] = 0;
+        for (int i = tid; i < gx * RB_S; i += RB_CH) bits[i] = 0;
         if (tid < gx) gb[tid] = cur.gbv;
         __syncthreads();
         const bool live = (uint32_t)tid < cur.n;
         const int x0 = (int)(cur.xr & 255u), x1 = (int)((cur.xr >> 8) & 255u);
         if (live)
-            for (int x = x0; x < x1; ++x) atomicOr(&bits[x * RB_W + wd], bit);
+            for (int x = x0; x < x1; ++x) atomicOr(&bits[x * RB_S + wd], bit);
         if (cur.s == 0 && tid < gx) {  // this row's tile ranges
             const uint32_t a = min(gb[tid], cap);
             uint32_t b;
@@ -347,7 +351,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
         const bool staged = tot <= (uint32_t)RB_STAGE;  // uniform
         if (live)
             for (int x = x0; x < x1; ++x) {
-                const uint32_t rank = pre[x * RB_W + wd] + (uint32_t)__popc(bits[x * RB_W + wd] & below);
+                const uint32_t rank = pre[x * RB_S + wd] + (uint32_t)__popc(bits[x * RB_S + wd] & below);
                 const uint32_t uu = cur.u + (uint32_t)(x - x0);
                 if (staged) {
                     const uint32_t lp = lst[x] + rank;
@@ -415,14 +419,14 @@ void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uin
         hipLaunchKernelGGL(k_rows_count, dim3(nch1), dim3(RB_CH), 0, st, P, gy, nch1, rect, table1, S1.base,
                            cdiv(S1.bytes, 16));
         launch_scan_exclusive(table1, base1, n1, nullptr, S1, st);
-        hipLaunchKernelGGL(k_rows_scatter, dim3(nch1), dim3(RB_CH), 2 * gy * RB_W * 4, st, P, gy, nch1, order,
+        hipLaunchKernelGGL(k_rows_scatter, dim3(nch1), dim3(RB_CH), 2 * gy * RB_S * 4, st, P, gy, nch1, order,
                            offsets, rect, base1, goff, e_gid, e_u, e_x, cap32);
     } else if (stage == 1) {  // level 2: tiles (+ ranges)
         const int grid2 = (int)std::min<size_t>(RB_GRID2, gy + cdiv(cap, RB_CH));
         hipLaunchKernelGGL(k_tiles_count, dim3(grid2), dim3(RB_CH), 0, st, gx, gy, nch1, table1, base1, e_x, table2,
                            len2, cap32, S2.base, cdiv(S2.bytes, 16), ranges);
         launch_scan_exclusive(table2, base2, n2, len2, S2, st);
-        hipLaunchKernelGGL(k_tiles_scatter, dim3(grid2), dim3(RB_CH), 2 * gx * RB_W * 4, st, gx, gy, nch1, table1,
+        hipLaunchKernelGGL(k_tiles_scatter, dim3(grid2), dim3(RB_CH), 2 * gx * RB_S * 4, st, gx, gy, nch1, table1,
                            base1, base2, e_gid, e_u, e_x, point_list, slot_vals, cap32, n_total, ranges, written,
                            written16);
     } else {  // heavy-first tile order (binning.hip)
