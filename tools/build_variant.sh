@@ -10,6 +10,7 @@ declare -A sub
 flags=()
 for a in "$@"; do
   case $a in
+    -*) flags+=("$a") ;;
     *=*) sub[${a%%=*}]=${a#*=} ;;
     *) flags+=("$a") ;;
   esac
