@@ -100,10 +100,6 @@ __device__ __forceinline__ float gsr_expf_nc(float x) {
 #define GSR_EXP_NC(x) gsr_expf_nc(x)
 #endif
 
-// Two pixels' powers at once: v_pk_add_f32 / v_pk_mul_f32 issue both elements for the
-// price of one instruction, element by element in IEEE fp32 (same bits as scalar).
-typedef float f2 __attribute__((ext_vector_type(2)));
-
 #ifdef GSR_STATS
 // Instrumented build (tools/render_stats.py): wave-uniform loop counters, 16 per
 // kernel (fwd at 0, bwd at 16): 0 visited, 1 near-skip, 2 prefiltered out, 3 full,

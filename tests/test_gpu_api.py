@@ -173,3 +173,22 @@ def test_speculative_stage_b_matches_exact(gpu_available):
     for got, ref in ((spec_big, ref_big), (spec_big2, ref_big), (spec_small, ref_small)):
         for k in ref:
             assert torch.equal(got[k], ref[k]), k
+
+
+def test_stream_copy_reference_kernel(gpu_available):
+    """gsr_stream_copy (bench.py's measured HBM copy rate) moves the bytes exactly for every
+    float4-per-thread variant, including a tail that is not a multiple of the block, and
+    rejects bad arguments."""
+    import torch
+    from diff_gaussian_rasterization import _C
+    n = 1_000_003 * 4  # floats: 16-B multiple, not a multiple of 256 threads * 4 float4
+    src = torch.randn(n, device="cuda")
+    st = torch.cuda.current_stream().cuda_stream
+    for u in (1, 2, 4):
+        dst = torch.full_like(src, float("nan"))
+        assert _C._lib.gsr_stream_copy(src.data_ptr(), dst.data_ptr(), n * 4, u, st) == 0
+        torch.cuda.synchronize()
+        assert torch.equal(src, dst)
+    dst = torch.empty_like(src)
+    assert _C._lib.gsr_stream_copy(src.data_ptr(), dst.data_ptr(), 12, 1, st) != 0  # not a multiple of 16
+    assert _C._lib.gsr_stream_copy(src.data_ptr(), dst.data_ptr(), 16, 3, st) != 0  # bad variant
