@@ -187,7 +187,8 @@ def _dev_f32(t, device, name, align=4):
 
 
 _BIN_GUESS = os.environ.get("GSR_BIN_GUESS", "1") != "0"
-_last_rendered = {}  # device -> num_rendered of the last forward (binning size guess)
+_last_rendered = {}  # device -> num_rendered of the recent forwards (binning size guess)
+_GUESS_WINDOW = 16   # a trainer cycling through a batch of views sees each view's count again
 
 
 def _ptr(t):
@@ -267,9 +268,12 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
         alpha = torch.empty(1, H, W, **f32)
         segment = torch.empty(NUM_CLASS, H, W, **f32)
         # The binning buffer depends on num_rendered, known only after the geometry
-        # stage; allocate a guess (the last count on this device + 15%) before it so
-        # that nothing but the render launches sits between the sync and the GPU.
-        cap = _last_rendered.get(device, 0)
+        # stage; allocate a guess (the largest of the recent counts on this device + 15%)
+        # before it so that nothing but the render launches sits between the sync and the
+        # GPU.  The largest, not the last: consecutive calls of a multi-view batch render
+        # different views, and a guess below the count costs an exact re-run of stage B.
+        recent = _last_rendered.get(device)
+        cap = max(recent) if recent else 0
         cap = cap + cap // 7 + 4096 if cap and _BIN_GUESS else 0
         binning = torch.empty(_lib.gsr_binning_bytes(cap), **u8) if cap else None
         # every call on a binning buffer uses the layout of its capacity (gsr.h); with a guess
@@ -282,7 +286,9 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
                               binning.numel() if binning is not None else 0, img.data_ptr(), color.data_ptr(),
                               depth.data_ptr(), alpha.data_ptr(), segment.data_ptr(), stream, ctypes.byref(nr))
         num_rendered = int(nr.value)
-        _last_rendered[device] = num_rendered
+        recent = _last_rendered.setdefault(device, [])
+        recent.append(num_rendered)
+        del recent[:-_GUESS_WINDOW]
         if rc == GSR_NEED_BINNING:  # no guess, or too small: stage B with the exact size
             binning = torch.empty(_lib.gsr_binning_bytes(num_rendered), **u8)
             s.binning_capacity = binning_capacity(binning)
