@@ -81,22 +81,28 @@ __device__ __forceinline__ uint32_t lb_lookback(uint64_t* col, size_t stride, in
     }
     return excl;
 }
-// The same, reading 8 predecessors per dependent step (one thread per column; used by
-// the radix scatter, where 256 digit columns walk back in parallel).
-__device__ __forceinline__ uint32_t lb_lookback8(uint64_t* col, size_t stride, int t) {
+// The same, reading N predecessors per dependent step (one thread per column; used by
+// the radix scatter, where 256 digit columns walk back in parallel).  N = 1, 2, 4, 8, 16,
+// 32 measured at the 1M-key depth sort: 87, 84, 83, 84, 87, 93 us -- the look-back loads,
+// not the chain length, are what a wider window costs.
+#ifndef GSR_LB_STEP
+#define GSR_LB_STEP 8
+#endif
+template <int N>
+__device__ __forceinline__ uint32_t lb_lookback_n(uint64_t* col, size_t stride, int t) {
     uint32_t excl = 0;
     int i = t - 1;
     while (true) {
-        uint64_t w[8];
+        uint64_t w[N];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < N; ++k) {
             const int j = i - k;
             w[k] = j >= 0 ? lb_load(col + (size_t)j * stride) : LB_PRE;
         }
         int consumed = 0;
         bool done = false, stall = false;
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
+        for (int k = 0; k < N; ++k) {
             if (done || stall) continue;
             const uint32_t f = (uint32_t)(w[k] >> 32);
             if (f == 0) {
@@ -480,7 +486,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
                 lb_store(col, LB_PRE | tot);
             } else {
                 lb_store(col + (size_t)t * RADIX, LB_AGG | tot);
-                excl = lb_lookback8(col, RADIX, t);
+                excl = lb_lookback_n<GSR_LB_STEP>(col, RADIX, t);
                 lb_store(col + (size_t)t * RADIX, LB_PRE | (excl + tot));
             }
             gbase[tid] = gstart + excl;
@@ -596,10 +602,6 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
 // tiles first turns it into a longest-processing-time-first scheduler (the
 // natural row-major order leaves the dense centre tiles for the end).  Order
 // within a bucket is arbitrary: it changes timing only, never a result.
-__device__ __forceinline__ uint32_t len_bucket(uint2 r) {
-    const uint32_t len = r.y - r.x;
-    return len ? 32 - __clz(len) : 0;
-}
 
 // Counters are private to each wave (LDS [wave][bucket]): a lane's atomic contends only
 // with its own wave's lanes inside one instruction.  Shared counters serialised across
@@ -649,6 +651,46 @@ __global__ void __launch_bounds__(ORDER_THREADS) k_tile_order(uint2* __restrict_
         const uint32_t b = len_bucket(ranges[t]);
         order[boff[b] + atomicAdd(&wcnt[wave][b], 1u)] = (uint32_t)t;
     }
+}
+
+// The same schedule when the non-empty buckets were counted upstream (row binning:
+// k_tiles_scatter adds each row's bucket counts into bw[0, 33)): one thread per tile over
+// many blocks instead of one block walking every tile twice (11-12 us at 8160 tiles,
+// latency-bound on one CU).  A wave's lanes that share a bucket are grouped by a 6-ballot
+// match and take one global atomic position per group (bw[64 + b]).  Empty tiles (bucket
+// 0, including rows the binning never visited) go last, so their count is not needed.
+__global__ void __launch_bounds__(256) k_tile_order_counted(const uint2* __restrict__ ranges, int T,
+                                                            uint32_t* bw, uint32_t* __restrict__ order) {
+    __shared__ uint32_t boff[33];
+    const int tid = threadIdx.x;
+    if (tid < 64) {  // heavy first: exclusive offsets over buckets 32, 31, ..., 1; then bucket 0
+        const uint32_t v = tid < 32 ? bw[32 - tid] : 0u;
+        uint32_t x = v;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if (tid >= o) x += y;
+        }
+        if (tid < 32) boff[32 - tid] = x - v;
+        if (tid == 31) boff[0] = x;
+    }
+    __syncthreads();
+    const int t = blockIdx.x * 256 + tid;
+    const bool valid = t < T;
+    const uint32_t b = valid ? len_bucket(ranges[t]) : 0u;
+    uint64_t peers = __ballot(valid);
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {  // buckets 0..32
+        const bool set = (b >> k) & 1u;
+        const uint64_t m = __ballot(set);
+        peers &= set ? m : ~m;
+    }
+    const uint64_t lt = lanemask_lt();
+    uint32_t base = 0;
+    if (valid && (peers & lt) == 0) base = atomicAdd(&bw[64 + b], (uint32_t)__popcll(peers));
+    const int leader = valid ? (int)__builtin_ctzll(peers) : 0;
+    base = (uint32_t)__shfl((int)base, leader, 64);
+    if (valid) order[boff[b] + base + (uint32_t)__popcll(peers & lt)] = (uint32_t)t;
 }
 
 }  // namespace
@@ -773,6 +815,13 @@ void launch_scan_exclusive(const uint32_t* src, uint32_t* out, size_t n, const u
     if (n == 0) return;
     hipLaunchKernelGGL(k_scan<false>, dim3(cdiv(n, SCAN_TILE)), dim3(SCAN_THREADS), 0, st, src, nullptr, n, out,
                        W.status, W.counter, nullptr, 0, n_dev);
+}
+
+void launch_tile_order_counted(const uint2* ranges, int T, uint32_t* bucket_words, uint32_t* order,
+                               hipStream_t st) {
+    if (T == 0) return;
+    hipLaunchKernelGGL(k_tile_order_counted, dim3((unsigned)cdiv((size_t)T, 256)), dim3(256), 0, st, ranges, T,
+                       bucket_words, order);
 }
 
 void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st) {

@@ -242,13 +242,15 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_count(int gx, int gy, int nch1,
                                                        const uint32_t* __restrict__ base1,
                                                        const uint32_t* __restrict__ e_x, uint32_t* __restrict__ table2,
                                                        uint32_t* __restrict__ len2, uint32_t cap, void* zero,
-                                                       size_t nzero16, uint2* __restrict__ ranges) {
+                                                       size_t nzero16, uint2* __restrict__ ranges,
+                                                       uint32_t* __restrict__ bucket_words) {
     __shared__ RowMap m;
     __shared__ int d[RB_MAXB + 1];
     __shared__ uint32_t e[RB_MAXB + 1];
     __shared__ uint32_t tot;
     zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH + threadIdx.x, (size_t)gridDim.x * RB_CH);  // scan-2 words
     for (int t = blockIdx.x * RB_CH + threadIdx.x; t < gx * gy; t += gridDim.x * RB_CH) ranges[t] = make_uint2(0u, 0u);
+    if (blockIdx.x == 0 && threadIdx.x < TILE_BUCKET_WORDS) bucket_words[threadIdx.x] = 0u;
     build_row_map(m, gy, nch1, table1, base1, cap);
     if (blockIdx.x == 0 && threadIdx.x == 0) *len2 = (uint32_t)gx * m.nch2;
     for (uint32_t c = blockIdx.x; c < m.nch2; c += gridDim.x) {
@@ -283,7 +285,8 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
                                                          uint32_t* __restrict__ point_list,
                                                          uint32_t* __restrict__ slot_vals, uint32_t cap,
                                                          const uint32_t* __restrict__ n_total,
-                                                         uint2* __restrict__ ranges, uint4* zero, size_t nzero16) {
+                                                         uint2* __restrict__ ranges, uint4* zero, size_t nzero16,
+                                                         uint32_t* __restrict__ bucket_words) {
     extern __shared__ uint32_t dyn[];
     uint32_t* bits = dyn;
     uint32_t* pre = dyn + gx * RB_S;
@@ -292,6 +295,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
     __shared__ uint32_t s_gid[RB_STAGE], s_u[RB_STAGE];
     __shared__ uint8_t s_x[RB_STAGE];
     __shared__ uint32_t tot;
+    __shared__ uint32_t s_bc[33];  // this row's tiles per schedule bucket (k_tile_order_counted)
     const int tid = threadIdx.x;
     for (size_t i = (size_t)blockIdx.x * RB_CH + tid; i < nzero16; i += (size_t)gridDim.x * RB_CH)
         zero[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -325,6 +329,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
         const int y = cur.y;
         for (int i = tid; i < gx * RB_S; i += RB_CH) bits[i] = 0;
         if (tid < gx) gb[tid] = cur.gbv;
+        if (tid < 33) s_bc[tid] = 0;
         __syncthreads();
         const bool live = (uint32_t)tid < cur.n;
         const int x0 = (int)(cur.xr & 255u), x1 = (int)((cur.xr >> 8) & 255u);
@@ -340,12 +345,16 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
                 b = nx < len2 ? base2[nx] : itot;
             }
             b = min(b, cap);
-            ranges[(size_t)y * gx + tid] = b > a ? make_uint2(a, b) : make_uint2(0u, 0u);
+            const uint2 rg = b > a ? make_uint2(a, b) : make_uint2(0u, 0u);
+            ranges[(size_t)y * gx + tid] = rg;
+            const uint32_t bk = len_bucket(rg);
+            if (bk) atomicAdd(&s_bc[bk], 1u);
         }
         const uint32_t cn = c + gridDim.x;
         Chunk nxt;
         if (cn < m.nch2) nxt = fetch(cn);  // in flight while this chunk is ranked
         __syncthreads();
+        if (cur.s == 0 && tid < 33 && s_bc[tid]) atomicAdd(&bucket_words[tid], s_bc[tid]);
         bucket_prefix(bits, gx, pre, cnt);
         lds_scan256(cnt, gx, lst, &tot);
         const bool staged = tot <= (uint32_t)RB_STAGE;  // uniform
@@ -392,7 +401,7 @@ size_t rows_bin_geom_ws_bytes(size_t P, int gy) {
 
 size_t rows_bin_ws_bytes(size_t cap) {
     const size_t n2 = (size_t)RB_MAXB * (RB_MAXB + cdiv(cap > 0 ? cap : 1, RB_CH));
-    return ALIGN + 2 * align_up(n2 * 4) + scan_ws_bytes(n2);
+    return ALIGN + align_up(TILE_BUCKET_WORDS * 4) + 2 * align_up(n2 * 4) + scan_ws_bytes(n2);
 }
 
 void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uint32_t* offsets, const uint32_t* rect,
@@ -410,9 +419,11 @@ void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uin
     const size_t n2 = (size_t)gx * (gy + cdiv(cap, RB_CH));  // table-2 entries bound
     char* bw = static_cast<char*>(bin_ws);
     uint32_t* len2 = reinterpret_cast<uint32_t*>(bw);
-    uint32_t* table2 = reinterpret_cast<uint32_t*>(bw + ALIGN);
-    uint32_t* base2 = reinterpret_cast<uint32_t*>(bw + ALIGN + align_up(n2 * 4));
-    void* scan2 = bw + ALIGN + 2 * align_up(n2 * 4);
+    uint32_t* bucket_words = reinterpret_cast<uint32_t*>(bw + ALIGN);
+    char* bw2 = bw + ALIGN + align_up(TILE_BUCKET_WORDS * 4);
+    uint32_t* table2 = reinterpret_cast<uint32_t*>(bw2);
+    uint32_t* base2 = reinterpret_cast<uint32_t*>(bw2 + align_up(n2 * 4));
+    void* scan2 = bw2 + 2 * align_up(n2 * 4);
     const ScanWs S2 = scan_ws(n2, scan2);
     const uint32_t cap32 = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
     if (stage == 0) {  // level 1: rows
@@ -424,13 +435,13 @@ void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uin
     } else if (stage == 1) {  // level 2: tiles (+ ranges)
         const int grid2 = (int)std::min<size_t>(RB_GRID2, gy + cdiv(cap, RB_CH));
         hipLaunchKernelGGL(k_tiles_count, dim3(grid2), dim3(RB_CH), 0, st, gx, gy, nch1, table1, base1, e_x, table2,
-                           len2, cap32, S2.base, cdiv(S2.bytes, 16), ranges);
+                           len2, cap32, S2.base, cdiv(S2.bytes, 16), ranges, bucket_words);
         launch_scan_exclusive(table2, base2, n2, len2, S2, st);
         hipLaunchKernelGGL(k_tiles_scatter, dim3(grid2), dim3(RB_CH), 2 * gx * RB_S * 4, st, gx, gy, nch1, table1,
                            base1, base2, e_gid, e_u, e_x, point_list, slot_vals, cap32, n_total, ranges, written,
-                           written16);
-    } else {  // heavy-first tile order (binning.hip)
-        launch_tile_order(ranges, gx * gy, tile_order, st);
+                           written16, bucket_words);
+    } else {  // heavy-first tile order from the bucket counts (binning.hip)
+        launch_tile_order_counted(ranges, gx * gy, bucket_words, tile_order, st);
     }
 }
 

@@ -36,6 +36,14 @@ __host__ __device__ inline size_t cdiv(size_t a, size_t b) { return (a + b - 1) 
 
 // Zero n4 16-B words with a grid-stride loop: lets a kernel that runs anyway clear
 // the next stage's counters instead of a separate memset launch.
+// Heavy-first tile schedule bucket: the bit length of a tile's instance count (0 = empty).
+__device__ __forceinline__ uint32_t len_bucket(uint2 r) {
+    const uint32_t len = r.y - r.x;
+    return len ? 32 - __clz(len) : 0;
+}
+// Bucket-count words of the row binning's tile order (k_tiles_scatter counts the non-empty
+// buckets, k_tile_order_counted ranks the tiles): counts at [0, 33), positions at [64, 97).
+constexpr int TILE_BUCKET_WORDS = 128;
 __device__ __forceinline__ void zero16(void* p, size_t n4, size_t tid, size_t nthreads) {
     uint4* q = static_cast<uint4*>(p);
     for (size_t i = tid; i < n4; i += nthreads) q[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -241,6 +249,8 @@ int sort_lb_items();
 bool sort_uses_lookback(size_t n);
 void set_sort_lookback_max(size_t n);
 void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st);
+// the same from bucket counts already taken (row binning): many blocks, no serial pass
+void launch_tile_order_counted(const uint2* ranges, int T, uint32_t* bucket_words, uint32_t* order, hipStream_t st);
 // value(j) = src[gather[j]] (gather != NULL), src[j], or, with rect_mode, the tile count
 // (x1 - x0)(y1 - y0) of the packed rect src[j]
 void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_idx, uint32_t* out, size_t n,
