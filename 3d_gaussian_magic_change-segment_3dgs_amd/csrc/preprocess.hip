@@ -501,42 +501,35 @@ __device__ __forceinline__ void sum_records(const float* __restrict__ contrib, c
     double d[12];
 #pragma unroll
     for (int j = 0; j < 12; ++j) d[j] = 0.0;
-    // Written flags (one byte per slot, 0 or 1) are read 32 at a time -- four 8-byte words
-    // whose loads are issued together -- and folded into a 32-bit mask (slot i -> bit i);
-    // then the written records of those 32 slots, four per round with their loads issued
-    // together (clamped slot indices: a record-at-a-time loop leaves one load in flight
-    // per lane).  A Gaussian covering many tiles thus costs one flag round trip per 32
-    // slots instead of one per 8 (the gather was 66 of the kernel's 143 us, most of it in
-    // the long ranges' serial round trips).  Sums stay in slot order.
-    const uint64_t* w8 = reinterpret_cast<const uint64_t*>(written);
-    const uint32_t wlo = lo >> 3, whi = (hi - 1) >> 3;
-    for (uint32_t w = wlo; w <= whi; w += 4) {
-        uint64_t f[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) f[k] = w8[min(w + (uint32_t)k, whi)];
-        uint32_t bits = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            uint32_t b = (uint32_t)(((f[k] & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
-            if (w + k == wlo) b &= 0xFFu << (lo & 7);
-            if (w + k == whi && ((hi & 7) != 0)) b &= ~(0xFFu << (hi & 7));
-            if (w + k > whi) b = 0;
-            bits |= b << (8 * k);
-        }
+    // Written flags (one byte per slot, 0 or 1) are read 32 at a time and folded into a
+    // 32-bit mask (slot base + i -> bit i); then the written records of those 32 slots, four
+    // per round with their loads issued together.  A Gaussian covering many tiles thus costs
+    // one flag round trip per 32 slots instead of one per 8 (the gather was 66 of the
+    // kernel's 143 us, most of it in the long ranges' serial round trips).  The record loads
+    // of a round's empty places are predicated off: clamped duplicates of the first record
+    // cost 6 us of address processing (0.1276 -> 0.1215 ms).  Sums stay in slot order.
+    auto fold8 = [](uint64_t f) {  // byte i of f (0 or 1) -> bit i
+        return (uint32_t)(((f & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56);
+    };
+    auto records = [&](uint32_t base, uint32_t bits) {
         while (bits) {
             uint32_t u[4];
             bool v[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 v[k] = bits != 0;
-                u[k] = v[k] ? (w << 3) + (uint32_t)__builtin_ctz(bits) : u[0];
+                u[k] = v[k] ? base + (uint32_t)__builtin_ctz(bits) : u[0];
                 bits &= bits - 1;
             }
             float4 r[4][3];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)u[k] * 12);
-                r[k][0] = src[0]; r[k][1] = src[1]; r[k][2] = src[2];
+                if (k == 0 || v[k]) {
+                    r[k][0] = src[0]; r[k][1] = src[1]; r[k][2] = src[2];
+                } else {
+                    r[k][0] = r[k][1] = r[k][2] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
             }
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -546,6 +539,21 @@ __device__ __forceinline__ void sum_records(const float* __restrict__ contrib, c
                 d[8] += r[k][2].x; d[9] += r[k][2].y; d[10] += r[k][2].z; d[11] += r[k][2].w;
             }
         }
+    };
+    // two 16-byte loads per 32 slots, from 16-slot granules (the flag array is 256-B aligned;
+    // four 8-byte loads from the range's first word took 0.8 us longer)
+    const uint4* w16 = reinterpret_cast<const uint4*>(written);
+    const uint32_t glo = lo >> 4, ghi = (hi - 1) >> 4;
+    for (uint32_t gi = glo; gi <= ghi; gi += 2) {
+        const uint4 f0 = w16[gi], f1 = w16[min(gi + 1, ghi)];
+        uint32_t bits = fold8((uint64_t)f0.x | ((uint64_t)f0.y << 32)) |
+                        fold8((uint64_t)f0.z | ((uint64_t)f0.w << 32)) << 8 |
+                        fold8((uint64_t)f1.x | ((uint64_t)f1.y << 32)) << 16 |
+                        fold8((uint64_t)f1.z | ((uint64_t)f1.w << 32)) << 24;
+        const uint32_t base = gi << 4;  // slot of bit 0; base <= hi - 1
+        if (lo > base) bits &= ~0u << (lo - base);              // lo - base < 16
+        if (hi - base < 32u) bits &= (1u << (hi - base)) - 1u;  // drops a clamped duplicate granule too
+        records(base, bits);
     }
 #pragma unroll
     for (int j = 0; j < 12; ++j) q[j] = (float)d[j];
