@@ -24,30 +24,6 @@ __device__ __forceinline__ uint64_t lanemask_lt() {
     return lane ? (~0ull >> (64 - lane)) : 0ull;
 }
 
-// Exclusive scan of one value per thread over a 256-thread block.
-// wsum: __shared__ uint32_t[4].  Returns the exclusive prefix; *total = block sum.
-__device__ __forceinline__ uint32_t block_exclusive_scan(uint32_t v, uint32_t* wsum, uint32_t* total) {
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t x = v;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t y = __shfl_up(x, o, 64);
-        if (lane >= o) x += y;
-    }
-    if (lane == 63) wsum[wid] = x;
-    __syncthreads();
-    uint32_t pre = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-        uint32_t s = wsum[w];
-        if (w < wid) pre += s;
-        tot += s;
-    }
-    __syncthreads();
-    *total = tot;
-    return pre + x - v;
-}
-
 // ------------------------------------------------- decoupled look-back ----
 // Single-pass prefix sums (scan, radix scatter) publish one 64-bit status word per
 // (tile, lane of the sum): flag in the high half (1 = tile aggregate, 2 = inclusive
@@ -178,7 +154,7 @@ __device__ __forceinline__ uint32_t block_exclusive_scan_w(uint32_t v, uint32_t*
 
 // ---------------------------------------------------------------- scan ----
 // out[i] = sum_{j<=i (INCLUSIVE) / j<i} value(j), value(j) = gather ? src[gather[j]] : src[j], in one
-// pass: each tile of 4096 values is staged through LDS (coalesced loads/stores),
+// pass: each tile of SCAN_TILE values is staged through LDS (coalesced loads/stores),
 // reduced, its prefix found by look-back, then scanned.
 // n_dev (optional): a device word; the scan then covers min(n, *n_dev) values (n sizes the
 // grid; tiles past the device count return at once -- no later tile depends on them).
@@ -189,7 +165,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restric
                                                        uint32_t* counter, uint32_t* host_total, int rect_mode,
                                                        const uint32_t* n_dev) {
     __shared__ uint32_t tile[SCAN_TILE + SCAN_TILE / 32];
-    __shared__ uint32_t wsum[4];
+    __shared__ uint32_t wsum[SCAN_THREADS / 64];
     __shared__ uint32_t s_excl;
     if (n_dev) n = min(n, (size_t)*n_dev);
     const int t = lb_tile_index(counter);
@@ -229,7 +205,7 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restric
         sum += v[i];
     }
     uint32_t total;
-    uint32_t pre = block_exclusive_scan(sum, wsum, &total);
+    uint32_t pre = block_exclusive_scan_w<SCAN_THREADS / 64>(sum, wsum, &total);
     if (threadIdx.x < 64) {  // wave 0: publish, look back over 64 tiles at a time, publish
         uint32_t excl = 0;
         if (t == 0) {

@@ -27,7 +27,16 @@ constexpr int REC_F4 = 4;
 
 // Radix sort / scan tiling (256-thread blocks = 4 wave64s, 16 items per thread).
 constexpr int SORT_THREADS = 256, SORT_ITEMS = 16, SORT_TILE = SORT_THREADS * SORT_ITEMS;
-constexpr int SCAN_THREADS = 256, SCAN_ITEMS = 16, SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
+// Look-back scan tiles of 8192 values, 16 waves x 8 per thread (r2, metric scene: the depth-
+// order scan 9.7 -> 8.4 us and the tile sort's level-2 scan ~4 us faster than 4 waves x 16;
+// tools/bench_stage_variants.sh with -DGSR_SCAN_THREADS / -DGSR_SCAN_ITEMS)
+#ifndef GSR_SCAN_THREADS
+#define GSR_SCAN_THREADS 1024
+#endif
+#ifndef GSR_SCAN_ITEMS
+#define GSR_SCAN_ITEMS 8
+#endif
+constexpr int SCAN_THREADS = GSR_SCAN_THREADS, SCAN_ITEMS = GSR_SCAN_ITEMS, SCAN_TILE = SCAN_THREADS * SCAN_ITEMS;
 constexpr int RADIX_BITS = 8, RADIX = 1 << RADIX_BITS;
 
 constexpr size_t ALIGN = 256;
