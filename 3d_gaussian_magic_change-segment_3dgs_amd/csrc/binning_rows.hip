@@ -36,7 +36,10 @@ namespace gsr {
 
 namespace {
 
-constexpr int RB_CH = 512;            // items per chunk = threads per block
+constexpr int RB_CH1 = 1024;          // level 1: depth-ordered Gaussians per chunk = threads per block
+constexpr int RB_S1 = RB_CH1 / 32 + 1; // its LDS words per bucket row (bitmask words + pad)
+constexpr int RB_STAGE1 = 4 * RB_CH1;  // its row entries assembled in LDS (more: direct writes)
+constexpr int RB_CH = 512;            // level 2: row entries per chunk = threads per block
 constexpr int RB_W = RB_CH / 32;      // bitmask words per bucket
 // LDS words per bucket row of bits / pre: one pad word so that the words of different
 // buckets fall in different banks (with a stride of 16 words, lanes touching buckets 4
@@ -78,21 +81,25 @@ __device__ void lds_scan256(const uint32_t* v, int n, uint32_t* out, uint32_t* t
 
 // bits[b * RB_S + w]: bit i of word w = item 32 w + i of the chunk covers bucket b.
 // pre[b * RB_S + w] = items of bucket b in words < w; cnt[b] = items of bucket b.
+// CH: items per chunk (= threads per block), CH / 32 bitmask words per bucket row of
+// CH / 32 + 1 LDS words.
+template <int CH>
 __device__ void bucket_prefix(const uint32_t* bits, int nb, uint32_t* pre, uint32_t* cnt) {
+    constexpr int W = CH / 32, S = W + 1;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int PER_WAVE = 64 / RB_W;  // buckets per wave pass
-    for (int b0 = PER_WAVE * wave; b0 < nb; b0 += PER_WAVE * (RB_CH / 64)) {
-        const int b = b0 + lane / RB_W, w = lane % RB_W;
-        const uint32_t c = b < nb ? (uint32_t)__popc(bits[b * RB_S + w]) : 0u;
+    constexpr int PER_WAVE = 64 / W;  // buckets per wave pass
+    for (int b0 = PER_WAVE * wave; b0 < nb; b0 += PER_WAVE * (CH / 64)) {
+        const int b = b0 + lane / W, w = lane % W;
+        const uint32_t c = b < nb ? (uint32_t)__popc(bits[b * S + w]) : 0u;
         uint32_t x = c;
 #pragma unroll
-        for (int o = 1; o < RB_W; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, o, RB_W);
+        for (int o = 1; o < W; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, W);
             if (w >= o) x += y;
         }
         if (b < nb) {
-            pre[b * RB_S + w] = x - c;
-            if (w == RB_W - 1) cnt[b] = x;
+            pre[b * S + w] = x - c;
+            if (w == W - 1) cnt[b] = x;
         }
     }
     __syncthreads();
@@ -106,16 +113,16 @@ __device__ __forceinline__ void unpack_rect(uint32_t pr, int& x0, int& y0, int& 
 }
 
 // ---------------------------------------------------------------- level 1 --
-// table1[y * nch1 + c] = Gaussians of chunk c (RB_CH depth-ordered Gaussians) covering row y.
-__global__ void __launch_bounds__(RB_CH) k_rows_count(int P, int gy, int nch1, const uint32_t* __restrict__ rect,
+// table1[y * nch1 + c] = Gaussians of chunk c (RB_CH1 depth-ordered Gaussians) covering row y.
+__global__ void __launch_bounds__(RB_CH1) k_rows_count(int P, int gy, int nch1, const uint32_t* __restrict__ rect,
                                                       uint32_t* __restrict__ table1, void* zero, size_t nzero16) {
     __shared__ int d[RB_MAXB + 1];
     __shared__ uint32_t e[RB_MAXB + 1];
     __shared__ uint32_t tot;
-    zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH + threadIdx.x, (size_t)gridDim.x * RB_CH);  // scan-1 words
-    for (int i = threadIdx.x; i <= gy; i += RB_CH) d[i] = 0;
+    zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH1 + threadIdx.x, (size_t)gridDim.x * RB_CH1);  // scan-1 words
+    for (int i = threadIdx.x; i <= gy; i += RB_CH1) d[i] = 0;
     __syncthreads();
-    const int r = blockIdx.x * RB_CH + threadIdx.x;
+    const int r = blockIdx.x * RB_CH1 + threadIdx.x;
     if (r < P) {
         int x0, y0, x1, y1;
         unpack_rect(rect[r], x0, y0, x1, y1);
@@ -126,14 +133,14 @@ __global__ void __launch_bounds__(RB_CH) k_rows_count(int P, int gy, int nch1, c
     }
     __syncthreads();
     lds_scan256(reinterpret_cast<const uint32_t*>(d), gy + 1, e, &tot);  // e[y + 1] = rows' counts
-    for (int y = threadIdx.x; y < gy; y += RB_CH) table1[(size_t)y * nch1 + blockIdx.x] = e[y + 1];
+    for (int y = threadIdx.x; y < gy; y += RB_CH1) table1[(size_t)y * nch1 + blockIdx.x] = e[y + 1];
 }
 
 // Level-1 entries (E1, grouped by row): e_gid = Gaussian id, e_u = its first instance slot
 // in the row, e_x = x0 | x1 << 8.  Also goff[gid] (the backward's record slots).
-// Dynamic LDS: bits + pre, 2 x gy x RB_S words (sized by the grid, not the 255 bound:
+// Dynamic LDS: bits + pre, 2 x gy x RB_S1 words (sized by the grid, not the 255 bound:
 // four blocks per CU at 1080p).  Every global load is issued before the first barrier.
-__global__ void __launch_bounds__(RB_CH) k_rows_scatter(int P, int gy, int nch1, const uint32_t* __restrict__ order,
+__global__ void __launch_bounds__(RB_CH1) k_rows_scatter(int P, int gy, int nch1, const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ rect,
                                                         const uint32_t* __restrict__ base1, uint32_t* __restrict__ goff,
@@ -141,12 +148,12 @@ __global__ void __launch_bounds__(RB_CH) k_rows_scatter(int P, int gy, int nch1,
                                                         uint32_t* __restrict__ e_x, uint32_t cap) {
     extern __shared__ uint32_t dyn[];
     uint32_t* bits = dyn;
-    uint32_t* pre = dyn + gy * RB_S;
+    uint32_t* pre = dyn + gy * RB_S1;
     __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
-    __shared__ uint32_t s_gid[RB_STAGE], s_u[RB_STAGE], s_x[RB_STAGE];
+    __shared__ uint32_t s_gid[RB_STAGE1], s_u[RB_STAGE1], s_x[RB_STAGE1];
     __shared__ uint32_t tot;
     const int tid = threadIdx.x;
-    const int r = blockIdx.x * RB_CH + tid;
+    const int r = blockIdx.x * RB_CH1 + tid;
     int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
     uint32_t g = 0, off = 0;
     if (r < P) {
@@ -154,22 +161,22 @@ __global__ void __launch_bounds__(RB_CH) k_rows_scatter(int P, int gy, int nch1,
         g = order[r];
         off = r == 0 ? 0u : offsets[r - 1];
     }
-    for (int i = tid; i < gy * RB_S; i += RB_CH) bits[i] = 0;
-    for (int y = tid; y < gy; y += RB_CH) gb[y] = base1[(size_t)y * nch1 + blockIdx.x];
+    for (int i = tid; i < gy * RB_S1; i += RB_CH1) bits[i] = 0;
+    for (int y = tid; y < gy; y += RB_CH1) gb[y] = base1[(size_t)y * nch1 + blockIdx.x];
     __syncthreads();
     const bool vis = x1 > x0 && y1 > y0;
     const uint32_t bit = 1u << (tid & 31), wd = (uint32_t)tid >> 5;
     if (vis)
-        for (int y = y0; y < y1; ++y) atomicOr(&bits[y * RB_S + wd], bit);
+        for (int y = y0; y < y1; ++y) atomicOr(&bits[y * RB_S1 + wd], bit);
     __syncthreads();
-    bucket_prefix(bits, gy, pre, cnt);
+    bucket_prefix<RB_CH1>(bits, gy, pre, cnt);
     lds_scan256(cnt, gy, lst, &tot);
-    const bool staged = tot <= (uint32_t)RB_STAGE;  // uniform
+    const bool staged = tot <= (uint32_t)RB_STAGE1;  // uniform
     if (vis) {
         goff[g] = off;
         const uint32_t w = (uint32_t)(x1 - x0), below = bit - 1u;
         for (int y = y0; y < y1; ++y) {
-            const uint32_t rank = pre[y * RB_S + wd] + (uint32_t)__popc(bits[y * RB_S + wd] & below);
+            const uint32_t rank = pre[y * RB_S1 + wd] + (uint32_t)__popc(bits[y * RB_S1 + wd] & below);
             const uint32_t u = off + (uint32_t)(y - y0) * w;
             const uint32_t xr = (uint32_t)x0 | ((uint32_t)x1 << 8) | ((uint32_t)y << 16);
             if (staged) {
@@ -189,7 +196,7 @@ __global__ void __launch_bounds__(RB_CH) k_rows_scatter(int P, int gy, int nch1,
     }
     if (!staged) return;
     __syncthreads();
-    for (uint32_t i = tid; i < tot; i += RB_CH) {
+    for (uint32_t i = tid; i < tot; i += RB_CH1) {
         const uint32_t xr = s_x[i], y = xr >> 16;
         const uint32_t gp = gb[y] + (i - lst[y]);
         if (gp < cap) {
@@ -355,7 +362,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
         if (cn < m.nch2) nxt = fetch(cn);  // in flight while this chunk is ranked
         __syncthreads();
         if (cur.s == 0 && tid < 33 && s_bc[tid]) atomicAdd(&bucket_words[tid], s_bc[tid]);
-        bucket_prefix(bits, gx, pre, cnt);
+        bucket_prefix<RB_CH>(bits, gx, pre, cnt);
         lds_scan256(cnt, gx, lst, &tot);
         const bool staged = tot <= (uint32_t)RB_STAGE;  // uniform
         if (live)
@@ -395,7 +402,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
 }  // namespace
 
 size_t rows_bin_geom_ws_bytes(size_t P, int gy) {
-    const size_t n1 = (size_t)gy * cdiv(P > 0 ? P : 1, RB_CH);
+    const size_t n1 = (size_t)gy * cdiv(P > 0 ? P : 1, RB_CH1);
     return 2 * align_up(n1 * 4) + scan_ws_bytes(n1);
 }
 
@@ -409,7 +416,7 @@ void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uin
                          uint32_t* point_list, uint32_t* slot_vals, uint2* ranges, uint32_t* tile_order,
                          uint4* written, size_t written16, size_t cap, const uint32_t* n_total, hipStream_t st,
                          int stage) {
-    const int nch1 = (int)cdiv(P, RB_CH);
+    const int nch1 = (int)cdiv(P, RB_CH1);
     const size_t n1 = (size_t)gy * nch1;
     char* gw = static_cast<char*>(geom_ws);
     uint32_t* table1 = reinterpret_cast<uint32_t*>(gw);
@@ -427,10 +434,10 @@ void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uin
     const ScanWs S2 = scan_ws(n2, scan2);
     const uint32_t cap32 = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
     if (stage == 0) {  // level 1: rows
-        hipLaunchKernelGGL(k_rows_count, dim3(nch1), dim3(RB_CH), 0, st, P, gy, nch1, rect, table1, S1.base,
+        hipLaunchKernelGGL(k_rows_count, dim3(nch1), dim3(RB_CH1), 0, st, P, gy, nch1, rect, table1, S1.base,
                            cdiv(S1.bytes, 16));
         launch_scan_exclusive(table1, base1, n1, nullptr, S1, st);
-        hipLaunchKernelGGL(k_rows_scatter, dim3(nch1), dim3(RB_CH), 2 * gy * RB_S * 4, st, P, gy, nch1, order,
+        hipLaunchKernelGGL(k_rows_scatter, dim3(nch1), dim3(RB_CH1), 2 * gy * RB_S1 * 4, st, P, gy, nch1, order,
                            offsets, rect, base1, goff, e_gid, e_u, e_x, cap32);
     } else if (stage == 1) {  // level 2: tiles (+ ranges)
         const int grid2 = (int)std::min<size_t>(RB_GRID2, gy + cdiv(cap, RB_CH));
