@@ -642,8 +642,13 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         float q[12];
         sum_records(contrib, written, lo_slot, lo_slot + n_slot, q);
         const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
+#ifdef GSR_MOMENT_MEAN
         const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * s.W);
         const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * s.H);
+#else
+        const float dm2x = -op * q[7] * (0.5f * s.W);  // q[7] = sum q (a dx + b dy)
+        const float dm2y = -op * q[8] * (0.5f * s.H);  // q[8] = sum q (b dx + c dy)
+#endif
         if (g.dmeans2D) { g.dmeans2D[i3] = dm2x; g.dmeans2D[i3 + 1] = dm2y; g.dmeans2D[i3 + 2] = 0.f; }
         if (g.dcolors) { g.dcolors[i3] = q[0]; g.dcolors[i3 + 1] = q[1]; g.dcolors[i3 + 2] = q[2]; }
         if (g.dopacity) g.dopacity[idx] = q[6];
@@ -907,8 +912,13 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, floa
         float q[12];
         sum_records(w.contrib, w.written, w.goff[idx], w.goff[idx] + w.tiles_touched[idx], q);
         const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
+#ifdef GSR_MOMENT_MEAN
         const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * w.W);
         const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * w.H);
+#else
+        const float dm2x = -op * q[7] * (0.5f * w.W);  // q[7] = sum q (a dx + b dy)
+        const float dm2y = -op * q[8] * (0.5f * w.H);  // q[8] = sum q (b dx + c dy)
+#endif
         if (w.dmeans2D) { w.dmeans2D[i3] = dm2x; w.dmeans2D[i3 + 1] = dm2y; w.dmeans2D[i3 + 2] = 0.f; }
         dcol = dcol + f3{q[0], q[1], q[2]};
         dop += q[6];

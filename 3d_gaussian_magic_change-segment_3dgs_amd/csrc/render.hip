@@ -126,6 +126,31 @@ extern "C" __attribute__((visibility("default"))) int gsr_stats_read(unsigned lo
 #define POPC(a) 0
 #endif
 
+#ifdef GSR_WAVE_TRACE
+// Timeline build (tools/wave_trace.py): per wave of the last launch of each render
+// kernel, {start, end} of s_memrealtime (100 MHz, chip-wide), the tile, its list length
+// and the last list position the wave visits, and the wave's HW_ID.
+__device__ unsigned long long g_gsr_wtrace[2][32768][4];
+extern "C" __attribute__((visibility("default"))) int gsr_wave_trace_read(unsigned long long* host) {
+    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gsr_wtrace), sizeof(g_gsr_wtrace)) == hipSuccess ? 0 : -1;
+}
+#define WT_BEGIN const unsigned long long wt0_ = __builtin_amdgcn_s_memrealtime();
+#define WT_END(kind, tile, n, depth)                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < 32768) {                                                     \
+        const unsigned long long wt1_ = __builtin_amdgcn_s_memrealtime();                             \
+        unsigned long long* w_ = g_gsr_wtrace[kind][blockIdx.x];                                      \
+        w_[0] = wt0_;                                                                                 \
+        w_[1] = wt1_;                                                                                 \
+        w_[2] = (unsigned long long)(tile) | ((unsigned long long)(unsigned)(n) << 32);               \
+        w_[3] = (unsigned long long)((unsigned)(depth) & 0xffffffu) |                                 \
+                ((unsigned long long)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 15u) << 24) | \
+                ((unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)) << 32); \
+    }
+#else
+#define WT_BEGIN
+#define WT_END(kind, tile, n, depth)
+#endif
+
 namespace gsr {
 namespace {
 
@@ -195,6 +220,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     // rounded exactly as the reference writes them (no contraction); only the
     // colour/depth/segment sums, which nothing amplifies, use explicit FMAs.
 #pragma clang fp contract(off)
+    WT_BEGIN
     const int tile = (int)order[blockIdx.x];
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
@@ -317,6 +343,7 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
         }
     }
     STAT_FLUSH(0)
+    WT_END(0, tile, n, (int)__builtin_amdgcn_readfirstlane(max(max(last[0], last[1]), max(last[2], last[3]))))
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
     const size_t HW = (size_t)H * W;
 #pragma unroll
@@ -378,22 +405,24 @@ __device__ __forceinline__ float wave_reduce12(float v[12], int lane, int& vidx,
     return r;
 }
 
-// q = num / den as num * v_rcp_f32(den) (<= 1.5 ulp; 2 VALU ops instead of the ~10 of
-// div_scale/fmas/fixup).  The replay divides T back through every contributor
-// (backward.cu:574); at the metric scene the gradients stay inside the reference's own
-// fp32 accumulation-order noise (profiles/round1_noise_rcpdiv.txt: dmeans2D 4.1e-7 vs
-// 3.1e-7, dscales 1.5e-6 vs 2.7e-6; the 1e-5 tolerance is untouched).  GSR_NEWTON_DIV adds
-// one Newton step (<= 1 ulp), GSR_IEEE_DIV uses the IEEE quotient.
+// q = num / den as v_rcp_f32 plus one Newton correction of the quotient (4 VALU ops
+// instead of the ~10 of div_scale/fmas/fixup; the corrected quotient is the correctly
+// rounded one except in rare cases).  The replay divides T back through every contributor
+// (backward.cu:574), so the quotient's rounding compounds along the pixel's list: with the
+// bare num * rcp(den) (<= 1.5 ulp per step, GSR_FAST_DIV) one element of dscales / drot of
+// C3 view 5 of 8 reached 1.2e-5 / 1.4e-5 of the tensor maximum (the reference's own
+// fp32-order noise there: 9e-6); with the correction 4.1e-6 / 5.4e-6, the same as the IEEE
+// quotient (GSR_IEEE_DIV, 50 us slower) (profiles/round3_div_study.txt).
 __device__ __forceinline__ float fdiv(float num, float den) {
 #if defined(GSR_IEEE_DIV)
     return num / den;
-#elif defined(GSR_NEWTON_DIV)
+#elif defined(GSR_FAST_DIV)
+    return num * __builtin_amdgcn_rcpf(den);
+#else
     const float r = __builtin_amdgcn_rcpf(den);
     const float q = num * r;
     const float e = __builtin_fmaf(-q, den, num);
     return __builtin_fmaf(e, r, q);
-#else
-    return num * __builtin_amdgcn_rcpf(den);
 #endif
 }
 
@@ -410,6 +439,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                                                    const float* __restrict__ dL_dalphas,
                                                    float* __restrict__ contrib, uint8_t* __restrict__ written) {
 #pragma clang fp contract(off)
+    WT_BEGIN
     const int tile = (int)order[blockIdx.x];
     const int lane = threadIdx.x;
     const int tx = tile % gx, ty = tile / gx;
@@ -576,10 +606,12 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                         near[k] & __builtin_amdgcn_ballot_w64(power[k] <= 0.0f) &
                         __builtin_amdgcn_ballot_w64(a >= ALPHA_MIN));
                     STAT(4, POPC(o));
-                    const float one_m = 1.f - a;
-                    const float Tn = fdiv(T[k], one_m);
-                    // a_m = alpha of a replayed pair, else 0: it masks dch and the Dk fold
+                    // a_m = alpha of a replayed pair, else 0: it masks dch and the Dk fold, and
+                    // makes Tn == T exactly off o (T / 1), so T needs no select; off o, a itself
+                    // may be anything (-inf * 0 would poison the quotient's correction step)
                     const float a_m = o ? a : 0.f;
+                    const float one_m = 1.f - a_m;
+                    const float Tn = fdiv(T[k], one_m);
                     const float dch_m = a_m * Tn;
                     float cdot = __builtin_fmaf(c0, dp0[k], da[k]);  // alpha channel (colour 1) first
                     cdot = __builtin_fmaf(c1, dp1[k], cdot);
@@ -609,11 +641,27 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                     // fold this contributor into the accumulators seen by the next one (front side)
                     // Dk' = a cdot + (1 - a) Dk, as Dk + a (cdot - Dk); unchanged when a_m = 0
                     Dk[k] = __builtin_fmaf(a_m, diff, Dk[k]);
-                    T[k] = o ? Tn : T[k];
+                    T[k] = Tn;
                 }
+#ifdef GSR_MOMENT_MEAN
                 acc[7] = dx * acc[6];   // sum q dx   (dx is shared by the lane's 4 pixels)
                 acc[9] = dx * acc[7];   // sum q dx^2
                 acc[10] = dx * acc[8];  // sum q dx dy
+#else
+                // The mean2D channels carry the conic-weighted sums per lane,
+                // sum q (a dx + b dy) and sum q (b dx + c dy), as the reference's per-pixel
+                // dG_ddelx / dG_ddely terms (backward.cu:612-621), instead of the moments
+                // Qx, Qy combined after the reduction: for an elongated Gaussian a Qx and
+                // b Qy nearly cancel, which amplified the moments' rounding ~100x there.
+                {
+                    const float qx = dx * acc[6];  // sum q dx (dx is shared by the lane's 4 pixels)
+                    const float qy = acc[8];
+                    acc[9] = dx * qx;              // sum q dx^2
+                    acc[10] = dx * qy;             // sum q dx dy
+                    acc[7] = __builtin_fmaf(ca, qx, cb * qy);
+                    acc[8] = __builtin_fmaf(cc, qy, cb * qx);
+                }
+#endif
                 int vidx;
                 bool valid;
                 const float r = wave_reduce12(acc, lane, vidx, valid);
@@ -629,6 +677,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     else
         replay(std::false_type{});
     STAT_FLUSH(16)
+    WT_END(1, tile, n, top0)
 }
 
 }  // namespace

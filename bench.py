@@ -53,12 +53,31 @@ PMC_SUMMARY = next((os.path.join(ROOT, "profiles", f) for f in ("round2_pmc_summ
                     if os.path.exists(os.path.join(ROOT, "profiles", f))), "")
 
 
+# {lib}: the collective library the process group actually runs on (dist.get_backend():
+# "nccl" is RCCL on ROCm, "gloo" the CPU rehearsal backend)
 EXCHANGE_DESC = {
-    "allreduce": "one RCCL all-reduce of the 61 f32/Gaussian grad bucket",
-    "sh": "SH exchange: RCCL all-gather of each view's 3-float dRGB rows + all-reduce of the 13 non-SH "
+    "allreduce": "one {lib} all-reduce of the 61 f32/Gaussian grad bucket",
+    "sh": "SH exchange: {lib} all-gather of each view's 3-float dRGB rows + all-reduce of the 13 non-SH "
           "f32/Gaussian, dsh rebuilt on every rank (gsr_tools.dp.ShExchange)",
     None: "",
 }
+
+
+def dist_info(dist):
+    """What the process group really is: backend name, world size and, for nccl, the
+    RCCL version torch was built against."""
+    if dist is None:
+        return {"backend": None, "world_size": 1, "collective_lib": None, "rccl_version": None}
+    backend = str(dist.get_backend())
+    ver = None
+    if backend == "nccl":
+        try:
+            v = torch.cuda.nccl.version()
+            ver = ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+        except Exception:
+            ver = None
+    return {"backend": backend, "world_size": int(dist.get_world_size()),
+            "collective_lib": "RCCL" if backend == "nccl" else backend, "rccl_version": ver}
 
 
 def algorithmic_bytes(stage, P, I, HW, deg, views=1, T=0):
@@ -130,7 +149,16 @@ def cpu_baseline(scene, cam, grads, budget_s=20.0):
     views(s1, c1, up1, 1)
     r1 = 20
     tf1, tb1 = views(s1, c1, up1, r1)
-    return {"value": round(reps / (tf + tb), 4), "unit": "views/s", "cores": int(O.lib().oracle_num_threads()),
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    threads = int(O.lib().oracle_num_threads())
+    return {"value": round(reps / (tf + tb), 4), "unit": "views/s", "cores": threads,
+            "cores_note": (f"OpenMP threads used = {threads} (OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}: "
+                           f"the pool's CPU share for one GPU); sched_getaffinity allows {affinity} of the "
+                           f"machine's os.cpu_count()={os.cpu_count()} logical CPUs, which other GPUs' jobs share"),
+            "affinity_cpus": affinity, "machine_cpus": os.cpu_count(),
             "kind": "port", "cpu_model": cpu_model(),
             "fwd_ms_per_view": round(1e3 * tf / reps, 1), "bwd_ms_per_view": round(1e3 * tb / reps, 1),
             "c1": {"value": round(r1 / (tf1 + tb1), 2), "unit": "views/s", "fwd_ms_per_view": round(1e3 * tf1 / r1, 2),
@@ -366,6 +394,7 @@ def main():
                                 "gbs": round(algorithmic_bytes(names[i], P, I, HW, deg, B, T=((W + 15) // 16) * ((H + 15) // 16))
                                              / (avg * 1e-3) / 1e9, 1)}
     dom = names[dom_i] if stages else None
+    dinfo = dist_info(dist)
     value = world * B * args.steps / elapsed
     roof = None
     if dom and cnt[dom_i]:
@@ -409,9 +438,12 @@ def main():
                                f"rank per step" + (" (per-view forward, one multi-view backward)" if B > 1 else
                                                    " through the drop-in GaussianRasterizer"), "P": P, "width": W, "height": H, "sh_degree": deg,
                    "num_classes": 2, "num_rendered": I, "global_batch": world * B, "views_per_step_per_gpu": B,
-                   "parallelism": f"dp{world}" + ((" (views sharded; " + EXCHANGE_DESC[step.exchange] +
+                   "parallelism": f"dp{world}" + ((" (views sharded; " +
+                                                   EXCHANGE_DESC[step.exchange].format(lib=dinfo["collective_lib"]) +
                                                    " per step, overlapped with the next step's render)")
-                                                  if world > 1 else "")},
+                                                  if world > 1 else ""),
+                   "dist_backend": dinfo["backend"], "world_size": dinfo["world_size"],
+                   "rccl_version": dinfo["rccl_version"]},
         "roofline": roof,
         "stages": stages,
     }

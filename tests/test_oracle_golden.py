@@ -89,3 +89,67 @@ def test_blend_exp_accuracy(oracle_mod):
     # outside the clamp: exp(-87) / exp(88) to within the same accuracy
     assert abs(oracle_mod.expf(-200.0) / math.exp(-87.0) - 1) < 1e-6
     assert abs(oracle_mod.expf(1000.0) / math.exp(88.0) - 1) < 1e-6
+
+
+# ---- utils/general_utils.py (tests/golden/general_utils_golden.npz) ----------------
+
+def _scene_of(means, scales, rots):
+    from gsr_tools.scene import Scene
+    N = means.shape[0]
+    return Scene(means, torch.zeros(N, 1, 3), torch.full((N, 1), 0.5), scales, rots, torch.full((N, 2), 0.5), 0)
+
+
+@pytest.mark.parametrize("tag,mod", [("1", 1.0), ("0p25", 0.25)])
+def test_oracle_cov3d_matches_reference_covariance(oracle_mod, tag, mod):
+    """Oracle cov3D (forward.cu:118-152: Sigma = (S R)^T (S R), S = diag(mod * s)) ==
+    the reference's Python covariance, strip_symmetric(L L^T) with L =
+    build_scaling_rotation(mod * s, q) (utils/general_utils.py:72-118 via
+    scene/gaussian_model.py:28-32), for normalised quaternions: the two evaluate the
+    same products in a different order, so they agree to a few fp32 ulps of the
+    covariance's largest entry."""
+    from gsr_tools.scene import make_camera, focal2fov
+    z = np.load(os.path.join(GOLD, "general_utils_golden.npz"))
+    scales = torch.from_numpy(z["scales"])
+    rots = torch.from_numpy(z["rotations_normalized"])
+    N = scales.shape[0]
+    g = torch.Generator().manual_seed(3)
+    means = (torch.rand(N, 3, generator=g) * 2 - 1) * 0.5  # in front of the camera: all preprocessed
+    cam = make_camera(np.eye(3), np.array([0.0, 0.0, 4.0]), 256, 256, focal2fov(200.0, 256), focal2fov(200.0, 256))
+    run = oracle_mod.run_scene(_scene_of(means, scales, rots), cam, scale_modifier=mod)
+    cov = run.get("cov3D").reshape(N, 6).astype(np.float64)
+    ref = z[f"cov3D_mod{tag}"].astype(np.float64)
+    # float64 truth of the same formula, to tell whose rounding the difference is
+    sd, qd = scales.double() * mod, rots.double()
+    w, x, y, zq = qd.T
+    R = torch.stack([1 - 2 * (y * y + zq * zq), 2 * (x * y - w * zq), 2 * (x * zq + w * y),
+                     2 * (x * y + w * zq), 1 - 2 * (x * x + zq * zq), 2 * (y * zq - w * x),
+                     2 * (x * zq - w * y), 2 * (y * zq + w * x), 1 - 2 * (x * x + y * y)], 1).view(N, 3, 3)
+    Lm = R @ torch.diag_embed(sd)
+    exact = (Lm @ Lm.transpose(1, 2))[:, [0, 0, 0, 1, 1, 2], [0, 1, 2, 1, 2, 2]].numpy()
+    scale = np.abs(exact).max(1, keepdims=True)
+    err = (np.abs(cov - ref) / scale).max()
+    err_oracle, err_ref = (np.abs(cov - exact) / scale).max(), (np.abs(ref - exact) / scale).max()
+    # measured: oracle vs reference 1.4e-6, oracle vs exact 4.0e-7, reference vs exact 1.3e-6
+    # (the reference's L L^T rounds more than the CUDA (SR)^T(SR) order the oracle follows)
+    assert err <= 2e-6, f"max |cov3D - reference| = {err:.2e} of the row's largest entry"
+    assert err_oracle <= max(err_ref, 5e-7), f"oracle {err_oracle:.2e} vs reference {err_ref:.2e} from float64"
+
+
+def test_train_oracle_build_rotation_matches_reference():
+    """oracle/train_oracle.py _build_rotation (used by densify_and_split) == the
+    reference's build_rotation (utils/general_utils.py:86-107), bitwise on the CPU."""
+    from oracle.train_oracle import _build_rotation
+    z = np.load(os.path.join(GOLD, "general_utils_golden.npz"))
+    np.testing.assert_array_equal(_build_rotation(torch.from_numpy(z["rotations"])).numpy(), z["build_rotation"])
+
+
+def test_lr_schedule_matches_reference():
+    """gsr_train.get_expon_lr_func == the reference's get_expon_lr_func
+    (utils/general_utils.py:37-70), bitwise (both float64 numpy)."""
+    from gsr_train.gaussian_model import get_expon_lr_func
+    z = np.load(os.path.join(GOLD, "general_utils_golden.npz"))
+    for i, (a, b, d, m, n) in enumerate(z["lr_cases"]):
+        f = get_expon_lr_func(lr_init=float(a), lr_final=float(b), lr_delay_steps=int(d), lr_delay_mult=float(m),
+                              max_steps=int(n))
+        got = np.array([float(f(int(s))) for s in z["lr_steps"]])
+        np.testing.assert_array_equal(got, z[f"lr_case{i}"], err_msg=f"case {i}")

@@ -1,0 +1,83 @@
+"""Wave timeline of the render kernels (build with -DGSR_WAVE_TRACE, e.g.
+tools/build_variant.sh wtrace -DGSR_WAVE_TRACE; run with GSR_LIBRARY pointing at it).
+
+Renders the metric scene (fwd + bwd) a few times, then reads, per wave of the last
+launch of k_render_fwd / k_render_bwd: start/end (s_memrealtime, 100 MHz), tile, list
+length, deepest list position visited, XCC and HW_ID.  Prints: span, waves alive over
+time (how full the chip is), the tail (time with fewer than half the wave slots busy),
+duration vs visited depth.  usage: python tools/wave_trace.py [config] [out.npz]"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd"), os.path.join(ROOT, "tests")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import harness as Hn  # noqa: E402
+from gsr_tools.scene import config_scene_and_camera  # noqa: E402
+
+
+def analyse(name, tr, ntiles, slots):
+    tr = tr[:ntiles]
+    t0, t1 = tr[:, 0].astype(np.int64), tr[:, 1].astype(np.int64)
+    ok = (t1 > 0) & (t0 > 0)
+    tr, t0, t1 = tr[ok], t0[ok], t1[ok]
+    base = t0.min()
+    s, e = (t0 - base) * 10, (t1 - base) * 10  # ns
+    span = e.max()
+    dur = e - s
+    n = (tr[:, 2] >> 32).astype(np.int64)
+    depth = (tr[:, 3] & 0xFFFFFF).astype(np.int64)
+    xcc = ((tr[:, 3] >> 24) & 15).astype(np.int64)
+    print(f"== {name}: {len(tr)} waves, span {span / 1e3:.1f} us, wave duration mean {dur.mean() / 1e3:.1f} us, "
+          f"max {dur.max() / 1e3:.1f} us, p50 {np.median(dur) / 1e3:.1f}, p90 {np.percentile(dur, 90) / 1e3:.1f}")
+    bins = np.arange(0, span + 1000, 1000)
+    alive = np.zeros(len(bins))
+    for i, b in enumerate(bins):
+        alive[i] = np.sum((s <= b) & (e > b))
+    print(f"   waves alive (per us): mean {alive.mean():.0f} of {slots} slots; "
+          f"time with < {slots // 2} alive: {np.mean(alive < slots // 2) * 100:.0f}% of the span; "
+          f"< {slots // 4}: {np.mean(alive < slots // 4) * 100:.0f}%")
+    q = np.linspace(0, len(bins) - 1, 11).astype(int)
+    print("   alive at 0..100% of span:", " ".join(f"{int(alive[i])}" for i in q))
+    last_start = s.max()
+    print(f"   last wave starts at {last_start / 1e3:.1f} us ({last_start / span * 100:.0f}% of span); "
+          f"start->end of the last 1% of waves: {np.sort(e)[-max(1, len(e) // 100)] / 1e3:.1f}..{span / 1e3:.1f} us")
+    # duration model: per visited position
+    if depth.max() > 0:
+        A = np.vstack([depth, np.ones_like(depth)]).T.astype(np.float64)
+        c, *_ = np.linalg.lstsq(A, dur.astype(np.float64), rcond=None)
+        print(f"   duration ~ {c[0]:.1f} ns x depth + {c[1] / 1e3:.2f} us; depth mean {depth.mean():.0f} "
+              f"max {depth.max()}, list n mean {n.mean():.0f} max {n.max()}")
+    print("   waves per XCC:", np.bincount(xcc, minlength=8).tolist())
+    return dict(start=s, end=e, depth=depth, n=n, xcc=xcc)
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "mt"
+    out = sys.argv[2] if len(sys.argv) > 2 else None
+    from diff_gaussian_rasterization import _C
+    lib = _C._lib
+    lib.gsr_wave_trace_read.argtypes = [ctypes.c_void_p]
+    scene, cam = config_scene_and_camera(cfg)
+    grads = Hn.upstream_grads(cam.height, cam.width)
+    for _ in range(4):
+        Hn.run_gsr(scene, cam, grads=grads, want_state=False)
+    torch.cuda.synchronize()
+    buf = np.zeros((2, 32768, 4), np.uint64)
+    assert lib.gsr_wave_trace_read(buf.ctypes.data) == 0
+    ntiles = ((cam.width + 15) // 16) * ((cam.height + 15) // 16)
+    props = torch.cuda.get_device_properties(0)
+    slots = props.multi_processor_count * 4 * 4  # 4 SIMDs per CU x 4 waves per SIMD (the kernels' cap)
+    res = {}
+    for k, name in enumerate(("k_render_fwd", "k_render_bwd")):
+        r = analyse(name, buf[k], ntiles, slots if k == 1 else props.multi_processor_count * 4 * 5)
+        res.update({f"{name}_{a}": v for a, v in r.items()})
+    if out:
+        np.savez_compressed(out, **res)
+
+
+if __name__ == "__main__":
+    main()
