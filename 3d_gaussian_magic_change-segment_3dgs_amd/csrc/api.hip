@@ -233,6 +233,14 @@ int gsr_set_option(const char* name, long long value) {
         g_rows_binning = value != 0;
         return 0;
     }
+    if (std::string(name) == "split_fwd_bucket") {  // render forward: tiles with n >= 2^(v-1) on two waves; 0 = off
+        gsr::set_split_buckets((int)value, -1);
+        return 0;
+    }
+    if (std::string(name) == "split_bwd_depth") {  // render backward: tiles this deep on two waves; 0 = off
+        gsr::set_split_buckets(-1, (int)value);
+        return 0;
+    }
     if (std::string(name) == "sort_lookback_max") {
         gsr::set_sort_lookback_max(value < 0 ? 0 : (size_t)value);
         return 0;
@@ -445,7 +453,7 @@ int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* b
     GSR_STAGE("tile order");
     {
         StageScope sc(GSR_STAGE_RENDER_FWD, st);
-        launch_render_forward(s->W, s->H, IL.gx, IL.gy, order, ranges, point_list,
+        launch_render_forward(s->W, s->H, IL.gx, IL.gy, order, order + T, ranges, point_list,
                               g ? at<float4>(g, GL.rec) : nullptr, s->bg, out_color, out_depth, out_alpha,
                               out_segment, at<uint32_t>(im, IL.n_contrib), st);
     }
@@ -511,7 +519,8 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
         written = at<uint8_t>(b, BL.written);  // cleared by the forward's tile sort
         {
             StageScope sc(GSR_STAGE_RENDER_BWD, st);
-            launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order), at<uint2>(im, IL.ranges),
+            launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order),
+                                   at<uint32_t>(im, IL.order) + IL.gx * IL.gy, at<uint2>(im, IL.ranges),
                                    at<uint32_t>(b, BL.point_list), at<uint32_t>(b, BL.slot_vals),
                                    at<float4>(g, GL.rec), s->bg, alpha, at<uint32_t>(im, IL.n_contrib), dL_dcolor,
                                    dL_dsegment, dL_ddepth, dL_dalpha, contrib, written, st);
@@ -582,7 +591,8 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
             {
                 StageScope sc(GSR_STAGE_RENDER_BWD, st);
                 launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order),
-                                       at<uint2>(im, IL.ranges), at<uint32_t>(b, BL.point_list),
+                                       at<uint32_t>(im, IL.order) + IL.gx * IL.gy, at<uint2>(im, IL.ranges),
+                                       at<uint32_t>(b, BL.point_list),
                                        at<uint32_t>(b, BL.slot_vals), at<float4>(g, GL.rec), s->bg, V.alpha,
                                        at<uint32_t>(im, IL.n_contrib), V.dL_dcolor, V.dL_dsegment, V.dL_ddepth,
                                        V.dL_dalpha, contrib, written, st);
@@ -705,6 +715,7 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
     else if (n == "slot_vals") B(BL.slot_vals, I * 4);
     else if (n == "ranges") M(IL.ranges, T * 8);
     else if (n == "n_contrib_tiles") M(IL.n_contrib, T * TILE_PIX * 4);
+    else if (n == "tile_order") M(IL.order, tile_sched_words(T) * 4);  // heavy-first order + TileSched
     else return -1;
     if (bytes == 0) return 0;
     if (!src) return -1;

@@ -584,11 +584,21 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
 // the whole block when most tiles share a bucket (at the 6M-Gaussian config every tile
 // length has the same bit length: 0.1 ms).
 constexpr int ORDER_THREADS = 1024, ORDER_WAVES = ORDER_THREADS / 64;
+// sched[SCHED_*] = tiles in length buckets >= the kernel's split bucket B (the heavy-first
+// order lists buckets 32, 31, ..., so that is bucket B - 1's offset); B = 0: no split.
+__device__ __forceinline__ void write_sched(uint32_t* sched, const uint32_t* boff, int split_fwd) {
+    sched[SCHED_FWD_SPLIT] = split_fwd > 0 && split_fwd <= 33 ? boff[split_fwd - 1] : 0u;
+}
 __global__ void __launch_bounds__(ORDER_THREADS) k_tile_order(uint2* __restrict__ ranges, int T,
-                                                              uint32_t* __restrict__ order) {
+                                                              uint32_t* __restrict__ order, int split_fwd) {
     __shared__ uint32_t wcnt[ORDER_WAVES][33];
     const int tid = threadIdx.x, wave = tid >> 6;
     for (int i = tid; i < ORDER_WAVES * 33; i += ORDER_THREADS) (&wcnt[0][0])[i] = 0;
+    {  // the forward's backward queue starts empty
+        const TileSched ts = tile_sched(order, T);
+        for (int i = tid; i < BQ_BUCKETS; i += ORDER_THREADS) ts.bq_cnt[i] = 0u;
+        for (int i = tid; i < T; i += ORDER_THREADS) ts.tdone[i] = 0u;
+    }
     __syncthreads();
 #pragma unroll 4
     for (int t = tid; t < T; t += ORDER_THREADS) {
@@ -622,6 +632,7 @@ __global__ void __launch_bounds__(ORDER_THREADS) k_tile_order(uint2* __restrict_
         if (tid < 33) boff[32 - tid] = x - v;
     }
     __syncthreads();
+    if (tid == 0) write_sched(order + T, boff, split_fwd);
 #pragma unroll 4
     for (int t = tid; t < T; t += ORDER_THREADS) {
         const uint32_t b = len_bucket(ranges[t]);
@@ -636,7 +647,8 @@ __global__ void __launch_bounds__(ORDER_THREADS) k_tile_order(uint2* __restrict_
 // match and take one global atomic position per group (bw[64 + b]).  Empty tiles (bucket
 // 0, including rows the binning never visited) go last, so their count is not needed.
 __global__ void __launch_bounds__(256) k_tile_order_counted(const uint2* __restrict__ ranges, int T,
-                                                            uint32_t* bw, uint32_t* __restrict__ order) {
+                                                            uint32_t* bw, uint32_t* __restrict__ order,
+                                                            int split_fwd) {
     __shared__ uint32_t boff[33];
     const int tid = threadIdx.x;
     if (tid < 64) {  // heavy first: exclusive offsets over buckets 32, 31, ..., 1; then bucket 0
@@ -651,6 +663,13 @@ __global__ void __launch_bounds__(256) k_tile_order_counted(const uint2* __restr
         if (tid == 31) boff[0] = x;
     }
     __syncthreads();
+    if (blockIdx.x == 0 && tid == 0) write_sched(order + T, boff, split_fwd);
+    {  // the forward's backward queue starts empty
+        const TileSched ts = tile_sched(order, T);
+        if (blockIdx.x == 0 && tid < BQ_BUCKETS) ts.bq_cnt[tid] = 0u;
+        const int t0 = blockIdx.x * 256 + tid;
+        if (t0 < T) ts.tdone[t0] = 0u;
+    }
     const int t = blockIdx.x * 256 + tid;
     const bool valid = t < T;
     const uint32_t b = valid ? len_bucket(ranges[t]) : 0u;
@@ -793,16 +812,31 @@ void launch_scan_exclusive(const uint32_t* src, uint32_t* out, size_t n, const u
                        W.status, W.counter, nullptr, 0, n_dev);
 }
 
+// Split buckets (gsr_set_option "split_fwd_bucket" / "split_bwd_bucket"): tiles whose
+// list length has at least this bit length (n >= 2^(B-1)) get two waves.
+#ifndef GSR_SPLIT_FWD
+#define GSR_SPLIT_FWD 0
+#endif
+#ifndef GSR_SPLIT_BWD_DEPTH
+#define GSR_SPLIT_BWD_DEPTH 0
+#endif
+static int g_split_fwd = GSR_SPLIT_FWD, g_split_bwd_depth = GSR_SPLIT_BWD_DEPTH;
+void set_split_buckets(int fwd_bucket, int bwd_depth) {
+    if (fwd_bucket >= 0) g_split_fwd = fwd_bucket;
+    if (bwd_depth >= 0) g_split_bwd_depth = bwd_depth;
+}
+int split_bwd_depth() { return g_split_bwd_depth; }
+
 void launch_tile_order_counted(const uint2* ranges, int T, uint32_t* bucket_words, uint32_t* order,
                                hipStream_t st) {
     if (T == 0) return;
     hipLaunchKernelGGL(k_tile_order_counted, dim3((unsigned)cdiv((size_t)T, 256)), dim3(256), 0, st, ranges, T,
-                       bucket_words, order);
+                       bucket_words, order, g_split_fwd);
 }
 
 void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st) {
     if (T == 0) return;
-    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ranges, T, order);
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ranges, T, order, g_split_fwd);
 }
 
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,

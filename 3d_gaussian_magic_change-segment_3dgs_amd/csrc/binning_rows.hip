@@ -138,8 +138,10 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_count(int P, int gy, int nch1, 
 
 // Level-1 entries (E1, grouped by row): e_gid = Gaussian id, e_u = its first instance slot
 // in the row, e_x = x0 | x1 << 8.  Also goff[gid] (the backward's record slots).
-// Dynamic LDS: bits + pre, 2 x gy x RB_S1 words (sized by the grid, not the 255 bound:
-// four blocks per CU at 1080p).  Every global load is issued before the first barrier.
+// Dynamic LDS: bits + pre, 2 x gy x RB_S1 words, sized by the grid rather than the 255
+// bound (gy = 68 at 1080p: 18 KB; 67 KB at gy = 255, covered by the 4080-px-tall case of
+// tests/test_gpu_parity.py::test_rows_binning_matches_radix_path).  Every global load is
+// issued before the first barrier.
 __global__ void __launch_bounds__(RB_CH1) k_rows_scatter(int P, int gy, int nch1, const uint32_t* __restrict__ order,
                                                         const uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ rect,

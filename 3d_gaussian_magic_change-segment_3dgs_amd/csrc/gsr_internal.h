@@ -171,6 +171,34 @@ inline BinLayout bin_layout(size_t I) {
 inline size_t scratch_bytes(size_t I) { return align_up(I * 12 * sizeof(float)) + ALIGN; }
 
 // ---- image buffer (reference ImageState, rasterizer_impl.cu:173-179) ----
+// After the T entries of the tile order (img buffer), the render schedule:
+//   sched[SCHED_WORDS]  written by the tile-order kernels: [SCHED_FWD_SPLIT] = how many of
+//                       the heaviest tiles the forward splits over two waves;
+//   bq_cnt[BQ_BUCKETS], bq_list[BQ_BUCKETS][T]: the backward's queue -- the forward files
+//                       every tile it rendered under its depth (deepest contributor, in
+//                       steps of BQ_STEP list positions) and the backward walks the buckets
+//                       deepest first;
+//   tdone[T]:           split forward tiles: sum over finished halves of (depth << 1) | 1.
+// bq_cnt and tdone are zeroed by the tile-order kernels.
+constexpr int SCHED_FWD_SPLIT = 0, SCHED_WORDS = 4;
+constexpr int BQ_BUCKETS = 64, BQ_STEP = 16;
+struct TileSched {
+    uint32_t *sched, *bq_cnt, *tdone, *bq_list;
+};
+__host__ __device__ inline TileSched tile_sched(uint32_t* order, int T) {
+    TileSched s;
+    s.sched = order + T;
+    s.bq_cnt = s.sched + SCHED_WORDS;
+    s.tdone = s.bq_cnt + BQ_BUCKETS;
+    s.bq_list = s.tdone + T;
+    return s;
+}
+inline size_t tile_sched_words(size_t T) { return T + SCHED_WORDS + BQ_BUCKETS + T + BQ_BUCKETS * T; }
+// depth (1-based deepest contributor) -> backward bucket; 0 = nothing to replay
+__host__ __device__ inline uint32_t depth_bucket(uint32_t d) {
+    const uint32_t b = (d + BQ_STEP - 1) / BQ_STEP;
+    return b < (uint32_t)BQ_BUCKETS ? b : (uint32_t)BQ_BUCKETS - 1;
+}
 struct ImgLayout {
     size_t ranges, n_contrib, order, bytes;
     int gx, gy;
@@ -184,7 +212,7 @@ inline ImgLayout img_layout(int W, int H) {
     auto take = [&](size_t bytes) { size_t r = o; o = align_up(o + bytes); return r; };
     L.ranges = take(T * 8);
     L.n_contrib = take(T * TILE_PIX * 4);  // tile-major: [tile][local pixel]
-    L.order = take(T * 4);                 // heavy-first tile schedule
+    L.order = take(tile_sched_words(T) * 4);  // heavy-first tile order + the render schedule (TileSched)
     L.bytes = o + ALIGN;
     return L;
 }
@@ -257,6 +285,12 @@ int depth_sort_passes();
 int sort_lb_items();
 bool sort_uses_lookback(size_t n);
 void set_sort_lookback_max(size_t n);
+// Both tile-order launchers also write order[T + SCHED_FWD_SPLIT]: the number of tiles in
+// length buckets >= the forward's split bucket (set_split_buckets; 0 = no split), and zero
+// the backward queue's counters (TileSched).  bwd_depth: the backward splits tiles whose
+// deepest contributor is at least this deep (0 = no split; a render.hip launch argument).
+void set_split_buckets(int fwd_bucket, int bwd_depth);
+int split_bwd_depth();
 void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st);
 // the same from bucket counts already taken (row binning): many blocks, no serial pass
 void launch_tile_order_counted(const uint2* ranges, int T, uint32_t* bucket_words, uint32_t* order, hipStream_t st);
@@ -281,16 +315,18 @@ void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, con
                       const ushort4* rect, const uint32_t* rect_sorted, int gx, uint32_t* tkeys,
                       uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, uint32_t cap, hipStream_t st);
 // render.hip
-void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
-                           const uint32_t* point_list,
-                           const float4* rec, const float* bg, float* out_color, float* out_depth,
-                           float* out_alpha, float* out_segment, uint32_t* n_contrib, hipStream_t st);
-void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
-                            const uint32_t* point_list,
-                            const uint32_t* slot_vals, const float4* rec, const float* bg, const float* alpha,
-                            const uint32_t* n_contrib, const float* dL_dcolor, const float* dL_dsegment,
-                            const float* dL_ddepth, const float* dL_dalpha, float* contrib, uint8_t* written,
-                            hipStream_t st);
+// sched = order + T (TileSched).  Forward grid 2T single-wave blocks in the heavy-first
+// order (split tiles first); backward grid T two-wave blocks over the forward's depth
+// queue, deepest first (tiles at least split_bwd_depth() deep on both waves of a block).
+void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
+                           const uint2* ranges, const uint32_t* point_list, const float4* rec, const float* bg,
+                           float* out_color, float* out_depth, float* out_alpha, float* out_segment,
+                           uint32_t* n_contrib, hipStream_t st);
+void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
+                            const uint2* ranges, const uint32_t* point_list, const uint32_t* slot_vals,
+                            const float4* rec, const float* bg, const float* alpha, const uint32_t* n_contrib,
+                            const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
+                            const float* dL_dalpha, float* contrib, uint8_t* written, hipStream_t st);
 
 uint32_t higher_msb(uint32_t n);
 

@@ -116,7 +116,7 @@ extern "C" __attribute__((visibility("default"))) int gsr_stats_read(unsigned lo
 #define STAT_DECL unsigned long long st_[16] = {};
 #define STAT(i, v) (st_[i] += (v))
 #define STAT_FLUSH(off)                                                          \
-    if (threadIdx.x == 0)                                                        \
+    if ((threadIdx.x & 63) == 0)                                                 \
         for (int i_ = 0; i_ < 16; ++i_) atomicAdd(&g_gsr_stats[(off) + i_], st_[i_]);
 #define POPC(a) __popcll(__ballot(a))
 #else
@@ -128,27 +128,35 @@ extern "C" __attribute__((visibility("default"))) int gsr_stats_read(unsigned lo
 
 #ifdef GSR_WAVE_TRACE
 // Timeline build (tools/wave_trace.py): per wave of the last launch of each render
-// kernel, {start, end} of s_memrealtime (100 MHz, chip-wide), the tile, its list length
-// and the last list position the wave visits, and the wave's HW_ID.
+// kernel, {start, end} of s_memrealtime (100 MHz, chip-wide), the tile, its list length,
+// the last list position the wave visits, XCC and HW_ID.  Entry = the wave's slot
+// (forward: block; backward: 2 * block + wave).
 __device__ unsigned long long g_gsr_wtrace[2][32768][4];
-extern "C" __attribute__((visibility("default"))) int gsr_wave_trace_read(unsigned long long* host) {
-    return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gsr_wtrace), sizeof(g_gsr_wtrace)) == hipSuccess ? 0 : -1;
+extern "C" __attribute__((visibility("default"))) int gsr_wave_trace_read(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gsr_wtrace), sizeof(g_gsr_wtrace)) != hipSuccess) return -1;
+    if (reset) {
+        void* d = nullptr;
+        if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_gsr_wtrace)) != hipSuccess) return -1;
+        if (hipMemset(d, 0, sizeof(g_gsr_wtrace)) != hipSuccess) return -1;
+    }
+    return 0;
 }
 #define WT_BEGIN const unsigned long long wt0_ = __builtin_amdgcn_s_memrealtime();
-#define WT_END(kind, tile, n, depth)                                                                 \
-    if (threadIdx.x == 0 && blockIdx.x < 32768) {                                                     \
+#define WT_END(kind, slot, tile, n, depth, mode)                                                        \
+    if ((threadIdx.x & 63) == 0 && (slot) < 32768) {                                                  \
         const unsigned long long wt1_ = __builtin_amdgcn_s_memrealtime();                             \
-        unsigned long long* w_ = g_gsr_wtrace[kind][blockIdx.x];                                      \
+        unsigned long long* w_ = g_gsr_wtrace[kind][slot];                                            \
         w_[0] = wt0_;                                                                                 \
         w_[1] = wt1_;                                                                                 \
-        w_[2] = (unsigned long long)(tile) | ((unsigned long long)(unsigned)(n) << 32);               \
+        w_[2] = (unsigned long long)(tile) | ((unsigned long long)(mode) << 24) |                    \
+                ((unsigned long long)(unsigned)(n) << 32);                                            \
         w_[3] = (unsigned long long)((unsigned)(depth) & 0xffffffu) |                                 \
                 ((unsigned long long)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 15u) << 24) | \
                 ((unsigned long long)__builtin_amdgcn_s_getreg((4) | (0 << 6) | (31 << 11)) << 32); \
     }
 #else
 #define WT_BEGIN
-#define WT_END(kind, tile, n, depth)
+#define WT_END(kind, slot, tile, n, depth, mode)
 #endif
 
 namespace gsr {
@@ -207,13 +215,38 @@ __device__ __forceinline__ bool tile_hit(float x, float y, float a, float b, flo
     return qmin <= -2.f * pm + margin;
 }
 
-__global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const uint32_t* __restrict__ order,
-                                                   const uint2* __restrict__ ranges,
-                                                   const uint32_t* __restrict__ point_list,
-                                                   const float4* __restrict__ rec, const float* __restrict__ bg,
-                                                   float* __restrict__ out_color, float* __restrict__ out_depth,
-                                                   float* __restrict__ out_alpha, float* __restrict__ out_segment,
-                                                   uint32_t* __restrict__ n_contrib) {
+// Forward of one tile (NQ = 4: all four 8x8 quadrants, one wave) or of half of it (NQ = 2:
+// quadrants q0, q0 + 1, i.e. the top or the bottom 16x8 half).  The schedule gives the
+// heaviest tiles (list length >= 2^(B-1) instances, B = the split bucket) two waves each:
+// a wave's time grows with the list positions it visits, and at the metric scene the
+// longest single-wave tiles ran 160-240 us of the 245-us launch, while the chip was less
+// than half busy for the last 37% of it (tools/wave_trace.py, profiles/round3_wave_trace.txt).
+// Every pixel is computed by the same code either way: results are bit-identical.
+// File a rendered tile under its depth in the backward's queue (TileSched).  A split
+// tile's halves finish independently: each adds (depth << 1) | 1 to the tile's word, so
+// the second to finish (odd old value) reads the other half's depth from the value its
+// own add returned -- one relaxed atomic, no fences (an acquire / release pair costs an
+// L2 write-back + invalidate on this multi-XCD part: the split forward ran 50% slower
+// with it).  Lane 0 only.
+__device__ __forceinline__ void publish_depth(const TileSched& ts, int T, int tile, bool half, uint32_t d) {
+    if (half) {
+        const uint32_t old = atomicAdd(&ts.tdone[tile], (d << 1) | 1u);
+        if (!(old & 1u)) return;  // first half: the second files the tile
+        d = max(d, old >> 1);
+    }
+    const uint32_t b = depth_bucket(d);
+    if (b == 0) return;  // nothing for the backward to replay
+    const uint32_t pos = atomicAdd(&ts.bq_cnt[b], 1u);
+    ts.bq_list[(size_t)b * T + pos] = (uint32_t)tile;
+}
+
+template <int NQ>
+__device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int tile, int q0, int wslot, const TileSched& ts,
+                                         const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list,
+                                         const float4* __restrict__ rec, const float* __restrict__ bg,
+                                         float* __restrict__ out_color, float* __restrict__ out_depth,
+                                         float* __restrict__ out_alpha, float* __restrict__ out_segment,
+                                         uint32_t* __restrict__ n_contrib, float4 (*srec)[4]) {
     // The backward recovers T from T_final = 1 - sum(alpha*T) (backward.cu:468) and
     // divides back through every contributor, which amplifies a last-bit difference
     // in the weight sum by 1/T_final.  power, alpha, T and the weight sum are therefore
@@ -221,35 +254,41 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     // colour/depth/segment sums, which nothing amplifies, use explicit FMAs.
 #pragma clang fp contract(off)
     WT_BEGIN
-    const int tile = (int)order[blockIdx.x];
-    const int lane = threadIdx.x;
+    constexpr int NR = NQ / 2;  // quadrant rows covered: 2 (whole tile) or 1 (half)
+    const int lane = threadIdx.x & 63;
     const int tx = tile % gx, ty = tile / gx;
+    const int r0 = q0 >> 1;     // first quadrant row
     // Lane l owns pixel (l & 7, l >> 3) of each 8x8 quadrant k of the tile (k & 1: right
     // half, k >> 1: bottom half).  Square quadrants are gated tighter than 16x4 strips:
     // 8.7% fewer (quadrant, Gaussian) blends at the metric scene (tools/render_stats.py).
+    // Quadrant kk of this wave is k = q0 + kk: column kk & 1, row r0 + (kk >> 1).
     const int px0 = tx * BX + (lane & 7), py0 = ty * BY + (lane >> 3);
     const float pfx[2] = {(float)px0, (float)(px0 + 8)};
-    const float pfy[2] = {(float)py0, (float)(py0 + 8)};
-    // live[k]: lanes whose pixel of quadrant k is inside the image and not terminated,
+    float pfy[NR];
+#pragma unroll
+    for (int rr = 0; rr < NR; ++rr) pfy[rr] = (float)(py0 + 8 * (r0 + rr));
+    // live[kk]: lanes whose pixel of quadrant kk is inside the image and not terminated,
     // kept as a wave mask in SGPRs (no per-pair VALU compare); T stays at its value at
     // termination, which is the T the output uses (forward.cu:355-357 breaks before T).
-    float T[4], C0[4], C1[4], C2[4], S0[4], S1[4], Dp[4], Wt[4];
-    uint32_t last[4];
-    uint64_t live[4];
+    float T[NQ], C0[NQ], C1[NQ], C2[NQ], S0[NQ], S1[NQ], Dp[NQ], Wt[NQ];
+    uint32_t last[NQ];
+    uint64_t live[NQ];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int kk = 0; kk < NQ; ++kk) {
+        const int k = q0 + kk;
         const int px = px0 + 8 * (k & 1), py = py0 + 8 * (k >> 1);
-        live[k] = __builtin_amdgcn_ballot_w64(px < W && py < H);
-        T[k] = 1.0f;
-        C0[k] = C1[k] = C2[k] = S0[k] = S1[k] = Dp[k] = Wt[k] = 0.f;
-        last[k] = 0;
+        live[kk] = __builtin_amdgcn_ballot_w64(px < W && py < H);
+        T[kk] = 1.0f;
+        C0[kk] = C1[kk] = C2[kk] = S0[kk] = S1[kk] = Dp[kk] = Wt[kk] = 0.f;
+        last[kk] = 0;
     }
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
     STAT_DECL
     STAT(7, n);
-    const float x0 = (float)(tx * BX), y0 = (float)(ty * BY);
-    const float x1 = (float)min(tx * BX + BX - 1, W - 1), y1 = (float)min(ty * BY + BY - 1, H - 1);
+    // prefilter rectangle: the pixels this wave owns
+    const float x0 = (float)(tx * BX), y0 = (float)(ty * BY + 8 * r0);
+    const float x1 = (float)min(tx * BX + BX - 1, W - 1), y1 = (float)min(ty * BY + 8 * (r0 + NR) - 1, H - 1);
 
     // Two-stage software pipeline over batches of 64 instances: while batch b is
     // blended, the records of batch b+1 and the ids of batch b+2 are in flight
@@ -257,7 +296,6 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     // The batch's records are parked in LDS and read back with a wave-uniform address
     // (a broadcast ds_read): the blend loop then spends no VALU issue slots on
     // v_readlane broadcasts.  One wave per block, so the barriers are free.
-    __shared__ float4 srec[64][4];
     const uint32_t* plist = point_list + range.x;
     const int nlast = max(n - 1, 0);  // list positions are clamped to the last one
     uint32_t g_next = n > 0 ? plist[min(lane, nlast)] : 0u;
@@ -265,7 +303,10 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
     if (n > 0) cur = fetch_batch(rec, g_next);
     if (n > 0) g_next = plist[min(64 + lane, nlast)];
     for (int base = 0; base < n; base += 64) {
-        if (!(live[0] | live[1] | live[2] | live[3])) break;
+        uint64_t any_live = 0;
+#pragma unroll
+        for (int kk = 0; kk < NQ; ++kk) any_live |= live[kk];
+        if (!any_live) break;
         const int cnt = min(64, n - base);
         STAT(5, 1);
         const Batch nxt = fetch_batch(rec, g_next);
@@ -273,7 +314,26 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
         const float4 ra = cur.a, rb = cur.b, rc = cur.c;
         cur = nxt;
         const float pmin = power_floor(rb.y);
+#ifndef GSR_NO_LIVE_RECT
+        // prefilter against the quadrants that still have live pixels (deep tiles end with a
+        // few live quadrants; their instances need not reach the others)
+        float lx0 = x0, lx1 = x1, ly0 = y0, ly1 = y1;
+        {
+            uint64_t cl = 0, cr = 0, rt = 0, rbm = 0;
+#pragma unroll
+            for (int kk = 0; kk < NQ; ++kk) {
+                if (kk & 1) cr |= live[kk]; else cl |= live[kk];
+                if (kk >> 1) rbm |= live[kk]; else rt |= live[kk];
+            }
+            if (!cl) lx0 = x0 + 8.f;
+            if (!cr) lx1 = fminf(x1, x0 + 7.f);
+            if (NR == 2 && !rt) ly0 = y0 + 8.f;
+            if (NR == 2 && !rbm) ly1 = fminf(y1, y0 + 7.f);
+        }
+        uint64_t todo = __ballot(lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, lx0, lx1, ly0, ly1));
+#else
         uint64_t todo = __ballot(lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1));
+#endif
         STAT(2, cnt - __popcll(todo));
         __syncthreads();  // previous batch's reads are done
         srec[lane][0] = ra;                                      // x, y, conic a, b
@@ -284,81 +344,128 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, const u
         while (todo) {
             const int j = (int)__builtin_ctzll(todo);
             todo &= todo - 1;
-            const float4 q0 = srec[j][0], q1 = srec[j][1];
-            const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
+            const float4 q0v = srec[j][0], q1v = srec[j][1];
+            const float gx_ = q0v.x, gy_ = q0v.y, ca = q0v.z, cb = q0v.w, cc = q1v.x, pm = q1v.y;
             // power = -0.5 (a dx dx + c dy dy) - b dx dy, rounded as forward.cu:349 writes
-            // it; the products are shared by the two quadrants of a column / row.
+            // it; the products are shared by the quadrants of a column / row.
             const float dx0 = gx_ - pfx[0], dx1 = gx_ - pfx[1];
-            const float dy0 = gy_ - pfy[0], dy1 = gy_ - pfy[1];
             const float ax[2] = {ca * dx0 * dx0, ca * dx1 * dx1}, bx[2] = {cb * dx0, cb * dx1};
-            const float cy[2] = {cc * dy0 * dy0, cc * dy1 * dy1}, dyv[2] = {dy0, dy1};
-            float power[4];
-            uint64_t near[4];  // per quadrant: live lanes within reach
+            float cy[NR], dyv[NR];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            for (int rr = 0; rr < NR; ++rr) {
+                const float dy = gy_ - pfy[rr];
+                cy[rr] = cc * dy * dy;
+                dyv[rr] = dy;
+            }
+            float power[NQ];
+            uint64_t near[NQ];  // per quadrant: live lanes within reach
+            uint64_t any_near = 0;
+#pragma unroll
+            for (int kk = 0; kk < NQ; ++kk) {
+#ifdef GSR_DEAD_SKIP
+                if (!live[kk]) {  // a finished quadrant: no power, no ballot
+                    near[kk] = 0;
+                    power[kk] = 0.f;
+                    continue;
+                }
+#endif
                 // -0.5 S is exact, so -(0.5 S) - B as one fma(-0.5, S, -B): the same bits
-                power[k] = __builtin_fmaf(-0.5f, ax[k & 1] + cy[k >> 1], -(bx[k & 1] * dyv[k >> 1]));
-                near[k] = __builtin_amdgcn_ballot_w64(power[k] >= pm) & live[k];
+                power[kk] = __builtin_fmaf(-0.5f, ax[kk & 1] + cy[kk >> 1], -(bx[kk & 1] * dyv[kk >> 1]));
+                near[kk] = __builtin_amdgcn_ballot_w64(power[kk] >= pm) & live[kk];
+                any_near |= near[kk];
             }
             STAT(0, 1);
-            if (!(near[0] | near[1] | near[2] | near[3])) {
+            if (!any_near) {
                 STAT(1, 1);
                 continue;
             }
             STAT(3, 1);
-            const float4 q2 = srec[j][2], q3 = srec[j][3];
-            const float op = q1.z, dep = q3.x, s0 = q1.w;
-            const float cr = q2.x, cg = q2.y, cbl = q2.z, s1 = q2.w;
+            const float4 q2v = srec[j][2], q3v = srec[j][3];
+            const float op = q1v.z, dep = q3v.x, s0 = q1v.w;
+            const float cr = q2v.x, cg = q2v.y, cbl = q2v.z, s1 = q2v.w;
             // in a VGPR once per pair: the per-quadrant v_cndmask below may read only one SGPR
             // (its lane mask), so a scalar contributor would be re-moved into a VGPR per quadrant
             uint32_t contributor = (uint32_t)(base + j + 1);
             asm volatile("" : "+v"(contributor));
-            // Quadrant k is blended only if one of its pixels can pass; the exact
+            // Quadrant kk is blended only if one of its pixels can pass; the exact
             // reference tests below decide per pixel.
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (!near[k]) continue;
+            for (int kk = 0; kk < NQ; ++kk) {
+                if (!near[kk]) continue;
                 STAT(8, 1);
-                // lanes of near[k] (live, power >= the opacity floor) are the only ones that
+                // lanes of near[kk] (live, power >= the opacity floor) are the only ones that
                 // can pass; every result below is used only under that mask
-                const float alpha = fminf(0.99f, op * GSR_EXP_NC(power[k]));
-                const uint64_t m_o = near[k] & __builtin_amdgcn_ballot_w64(power[k] <= 0.0f) &
+                const float alpha = fminf(0.99f, op * GSR_EXP_NC(power[kk]));
+                const uint64_t m_o = near[kk] & __builtin_amdgcn_ballot_w64(power[kk] <= 0.0f) &
                                      __builtin_amdgcn_ballot_w64(alpha >= ALPHA_MIN);
-                const float test_T = T[k] * (1.f - alpha);
+                const float test_T = T[kk] * (1.f - alpha);
                 const uint64_t m_done = m_o & __builtin_amdgcn_ballot_w64(test_T < T_MIN);  // forward.cu:355-357
-                live[k] &= ~m_done;
+                live[kk] &= ~m_done;
                 const bool ok = __builtin_amdgcn_inverse_ballot_w64(m_o & ~m_done);
                 STAT(4, POPC(ok));
-                const float aT = (ok ? alpha : 0.f) * T[k];
-                C0[k] = __builtin_fmaf(cr, aT, C0[k]);
-                C1[k] = __builtin_fmaf(cg, aT, C1[k]);
-                C2[k] = __builtin_fmaf(cbl, aT, C2[k]);
-                Wt[k] += aT;  // weight += alpha * T (forward.cu:364), exact rounding
-                Dp[k] = __builtin_fmaf(dep, aT, Dp[k]);
-                S0[k] = __builtin_fmaf(s0, aT, S0[k]);
-                S1[k] = __builtin_fmaf(s1, aT, S1[k]);
-                T[k] = ok ? test_T : T[k];
-                last[k] = ok ? contributor : last[k];
+                const float aT = (ok ? alpha : 0.f) * T[kk];
+                C0[kk] = __builtin_fmaf(cr, aT, C0[kk]);
+                C1[kk] = __builtin_fmaf(cg, aT, C1[kk]);
+                C2[kk] = __builtin_fmaf(cbl, aT, C2[kk]);
+                Wt[kk] += aT;  // weight += alpha * T (forward.cu:364), exact rounding
+                Dp[kk] = __builtin_fmaf(dep, aT, Dp[kk]);
+                S0[kk] = __builtin_fmaf(s0, aT, S0[kk]);
+                S1[kk] = __builtin_fmaf(s1, aT, S1[kk]);
+                T[kk] = ok ? test_T : T[kk];
+                last[kk] = ok ? contributor : last[kk];
             }
         }
     }
     STAT_FLUSH(0)
-    WT_END(0, tile, n, (int)__builtin_amdgcn_readfirstlane(max(max(last[0], last[1]), max(last[2], last[3]))))
+    uint32_t deepest = 0;
+#pragma unroll
+    for (int kk = 0; kk < NQ; ++kk) deepest = max(deepest, last[kk]);
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) deepest = max(deepest, (uint32_t)__shfl_xor((int)deepest, o, 64));
+    if (lane == 0) publish_depth(ts, ntiles, tile, NQ != 4, deepest);
+    WT_END(0, wslot, tile, n, deepest, NQ)
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
     const size_t HW = (size_t)H * W;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        n_contrib[(size_t)tile * TILE_PIX + k * 64 + lane] = last[k];
+    for (int kk = 0; kk < NQ; ++kk) {
+        const int k = q0 + kk;
+        n_contrib[(size_t)tile * TILE_PIX + k * 64 + lane] = last[kk];
         const int px = px0 + 8 * (k & 1), py = py0 + 8 * (k >> 1);
         if (!(px < W && py < H)) continue;
         const size_t pix = (size_t)py * W + px;
-        out_color[pix] = C0[k] + T[k] * bg0;
-        out_color[HW + pix] = C1[k] + T[k] * bg1;
-        out_color[2 * HW + pix] = C2[k] + T[k] * bg2;
-        out_alpha[pix] = Wt[k];
-        out_depth[pix] = Dp[k];
-        out_segment[pix] = S0[k];
-        out_segment[HW + pix] = S1[k];
+        out_color[pix] = C0[kk] + T[kk] * bg0;
+        out_color[HW + pix] = C1[kk] + T[kk] * bg1;
+        out_color[2 * HW + pix] = C2[kk] + T[kk] * bg2;
+        out_alpha[pix] = Wt[kk];
+        out_depth[pix] = Dp[kk];
+        out_segment[pix] = S0[kk];
+        out_segment[HW + pix] = S1[kk];
+    }
+}
+
+// Block b < 2 Hs: half (b & 1) of heavy tile order[b >> 1] (the first Hs entries of the
+// heavy-first schedule, sched[0], written by the tile-order kernel); then one wave per
+// remaining tile.  The grid is sized for Hs = T; blocks past the work return at once.
+__global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, int T, const uint32_t* __restrict__ order,
+                                                   uint32_t* __restrict__ sched,
+                                                   const uint2* __restrict__ ranges,
+                                                   const uint32_t* __restrict__ point_list,
+                                                   const float4* __restrict__ rec, const float* __restrict__ bg,
+                                                   float* __restrict__ out_color, float* __restrict__ out_depth,
+                                                   float* __restrict__ out_alpha, float* __restrict__ out_segment,
+                                                   uint32_t* __restrict__ n_contrib) {
+    __shared__ float4 srec[64][4];
+    const TileSched ts = tile_sched(sched - T, T);
+    const uint32_t Hs = min(sched[SCHED_FWD_SPLIT], (uint32_t)T);
+    const uint32_t b = blockIdx.x;
+    if (b < 2 * Hs) {
+        fwd_tile<2>(W, H, gx, T, (int)order[b >> 1], 2 * (int)(b & 1), (int)b, ts, ranges, point_list, rec, bg,
+                    out_color, out_depth, out_alpha, out_segment, n_contrib, srec);
+    } else {
+        const uint32_t i = b - Hs;
+        if (i >= (uint32_t)T) return;
+        fwd_tile<4>(W, H, gx, T, (int)order[i], 0, (int)b, ts, ranges, point_list, rec, bg, out_color, out_depth,
+                    out_alpha, out_segment, n_contrib, srec);
     }
 }
 
@@ -426,25 +533,46 @@ __device__ __forceinline__ float fdiv(float num, float den) {
 #endif
 }
 
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_render_bwd(int W, int H, int gx, const uint32_t* __restrict__ order,
-                                                   const uint2* __restrict__ ranges,
-                                                   const uint32_t* __restrict__ point_list,
-                                                   const uint32_t* __restrict__ slot_vals,
-                                                   const float4* __restrict__ rec, const float* __restrict__ bg,
-                                                   const float* __restrict__ alphas,
-                                                   const uint32_t* __restrict__ n_contrib,
-                                                   const float* __restrict__ dL_dpixels,
-                                                   const float* __restrict__ dL_dsegs,
-                                                   const float* __restrict__ dL_ddepths,
-                                                   const float* __restrict__ dL_dalphas,
-                                                   float* __restrict__ contrib, uint8_t* __restrict__ written) {
+// LDS of one backward block (two waves): each wave parks its own copy of the batch
+// records; split tiles also exchange their per-wave partial records and the batch count.
+struct BwdShared {
+    float4 srec[2][64][4];  // per wave: the batch's records
+    float part[2][64][12];  // split tiles: per-wave partial record of each batch instance
+    uint64_t tmask[2];      // split tiles: instances each wave produced a partial for
+    uint32_t top[2];        // split tiles: per-wave deepest contributor | use_bg << 31
+};
+
+// LDS write -> read by other lanes of the SAME wave: a wave's LDS instructions execute in
+// order, so a compiler barrier plus the LDS counter wait is enough (no s_barrier: in the
+// unsplit mode the block's other wave renders another tile, or has already ended).
+__device__ __forceinline__ void wave_lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+// Backward of one tile (NS = 4 strips of 16x4 pixels, one wave) or of half of it (NS = 2:
+// strips s0, s0 + 1 = the top or the bottom 16x8 half, SPLIT: the block's two waves
+// cooperate on one tile).  A split tile's two waves walk the same batches (the deeper of
+// the halves' last contributors bounds both); per batch each wave reduces its partial
+// record of an instance into LDS, and after a block barrier the block sums the two
+// partials in a fixed order (wave 0 + wave 1: deterministic) and stores the record.
+template <int NS, bool SPLIT>
+__device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0, int wslot,
+                                         const uint2* __restrict__ ranges,
+                                         const uint32_t* __restrict__ point_list,
+                                         const uint32_t* __restrict__ slot_vals,
+                                         const float4* __restrict__ rec, const float* __restrict__ bg,
+                                         const float* __restrict__ alphas,
+                                         const uint32_t* __restrict__ n_contrib,
+                                         const float* __restrict__ dL_dpixels,
+                                         const float* __restrict__ dL_dsegs,
+                                         const float* __restrict__ dL_ddepths,
+                                         const float* __restrict__ dL_dalphas,
+                                         float* __restrict__ contrib, uint8_t* __restrict__ written,
+                                         float4 (*srec)[4], BwdShared* sh) {
 #pragma clang fp contract(off)
     WT_BEGIN
-    const int tile = (int)order[blockIdx.x];
-    const int lane = threadIdx.x;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int tx = tile % gx, ty = tile / gx;
     const int px = tx * BX + (lane & 15);
-    const int py0 = ty * BY + (lane >> 4);
+    const int py0 = ty * BY + (lane >> 4) + 4 * s0;
     const float pfx = (float)px;
     const size_t HW = (size_t)H * W;
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
@@ -458,18 +586,18 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     // reference's sum_ch (c[ch] - accum_rec[ch]) * dL_dch is cdot - Dk.  Equal in exact
     // arithmetic; the fp32 rounding differs from the per-channel form at the 1e-7
     // level (tests/test_gpu_parity.py tolerances), and 24 registers per lane are freed.
-    float pfy[4], T[4], Tfin[4], dp0[4], dp1[4], dp2[4], ds0[4], ds1[4], dd[4], da[4], bgdot[4];
-    float Dk[4];
-    uint32_t lastc[4];
+    float pfy[NS], T[NS], Tfin[NS], dp0[NS], dp1[NS], dp2[NS], ds0[NS], ds1[NS], dd[NS], da[NS], bgdot[NS];
+    float Dk[NS];
+    uint32_t lastc[NS];
     uint32_t maxlast = 0;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
+    for (int k = 0; k < NS; ++k) {
         const int py = py0 + 4 * k;
         pfy[k] = (float)py;
         const bool inside = px < W && py < H;
         const size_t pix = inside ? (size_t)py * W + px : 0;
         // n_contrib is in the forward's quadrant layout (entry 64 k' + 8 (row & 7) + (col & 7))
-        const int r = (lane >> 4) + 4 * k, c = lane & 15;
+        const int r = (lane >> 4) + 4 * (s0 + k), c = lane & 15;
         const int fidx = 64 * (2 * (r >> 3) + (c >> 3)) + 8 * (r & 7) + (c & 7);
         lastc[k] = inside ? n_contrib[(size_t)tile * TILE_PIX + fidx] : 0u;
         Tfin[k] = inside ? 1.f - alphas[pix] : 0.f;
@@ -491,20 +619,30 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) maxlast = max(maxlast, (uint32_t)__shfl_xor((int)maxlast, o, 64));
-    const bool use_bg = wave_any(bgdot[0] != 0.f || bgdot[1] != 0.f || bgdot[2] != 0.f || bgdot[3] != 0.f);
+    bool any_bg = false;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) any_bg |= bgdot[k] != 0.f;
+    bool use_bg = wave_any(any_bg);
+    int top0 = (int)__builtin_amdgcn_readfirstlane(maxlast);
+    if constexpr (SPLIT) {  // both waves walk the same batches (their barriers pair up)
+        if (lane == 0) sh->top[wid] = (uint32_t)top0 | (use_bg ? 0x80000000u : 0u);
+        __syncthreads();
+        const uint32_t t0 = sh->top[0], t1 = sh->top[1];
+        top0 = (int)max(t0 & 0x7FFFFFFFu, t1 & 0x7FFFFFFFu);
+        use_bg = ((t0 | t1) >> 31) != 0;
+    }
 
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
-    const float x0 = (float)(tx * BX), y0 = (float)(ty * BY);
-    const float x1 = (float)min(tx * BX + BX - 1, W - 1), y1 = (float)min(ty * BY + BY - 1, H - 1);
+    // prefilter rectangle: the pixels this wave owns
+    const float x0 = (float)(tx * BX), y0 = (float)(ty * BY + 4 * s0);
+    const float x1 = (float)min(tx * BX + BX - 1, W - 1), y1 = (float)min(ty * BY + 4 * (s0 + NS) - 1, H - 1);
 
     STAT_DECL
     STAT(7, n);
-    STAT(6, n > (int)maxlast ? n - (int)maxlast : 0);
+    STAT(6, n > top0 ? n - top0 : 0);
     // Same two-stage batch pipeline and LDS record broadcast as the forward, walking
     // the list back to front: lane l of the batch with upper end `top` owns position top-1-l.
-    __shared__ float4 srec[64][4];
-    const int top0 = (int)__builtin_amdgcn_readfirstlane(maxlast);
     const uint32_t* plist = point_list + range.x;
     const uint32_t* slist = slot_vals + range.x;
     // list positions below 0 are clamped to 0 (unconditional loads, see fetch_batch)
@@ -536,66 +674,86 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
             cur = nxt;
             u_cur = u_nxt;
             const float pmin = power_floor(rb.y);
-            const bool hit = lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1);
-            uint64_t todo = __ballot(hit);
             // Lanes replaying every position of this batch (p < n_contrib for all p < top) and
             // whether any lane starts replaying inside it: only then is p < n_contrib
-            // tested per instance.
-            uint64_t act_all[4];
+            // tested per instance.  Strips with no pixel replaying any position of the batch
+            // are idle: no powers for them, and the prefilter rectangle shrinks to the rows of
+            // the active strips (deep tiles start with few pixels replaying).
+            uint64_t act_all[NS];
             bool varying = false;
-    #pragma unroll
-            for (int k = 0; k < 4; ++k) {
+            uint32_t active = 0;  // bit k: strip k has a pixel replaying in this batch
+#pragma unroll
+            for (int k = 0; k < NS; ++k) {
                 act_all[k] = __builtin_amdgcn_ballot_w64(lastc[k] >= (uint32_t)top);
                 varying |= lastc[k] < (uint32_t)top && lastc[k] > (uint32_t)(top - cnt);
+                if (__builtin_amdgcn_ballot_w64(lastc[k] > (uint32_t)(top - cnt))) active |= 1u << k;
             }
             const bool vary = wave_any(varying);
+#ifndef GSR_NO_LIVE_RECT
+            const int kmin = active ? __builtin_ctz(active) : 0, kmax = active ? 31 - __builtin_clz(active) : 0;
+            const float ay0 = y0 + 4.f * kmin, ay1 = fminf(y1, y0 + 4.f * kmax + 3.f);
+            const bool hit = lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, ay0, ay1);
+#else
+            const bool hit = lane < cnt && tile_hit(ra.x, ra.y, ra.z, ra.w, rb.x, pmin, x0, x1, y0, y1);
+#endif
+            uint64_t todo = __ballot(hit);
             STAT(9, vary);
             STAT(2, cnt - __popcll(todo));
-            __syncthreads();  // previous batch's reads are done
+            wave_lds_sync();  // this wave's reads of the previous batch are issued before the writes
             srec[lane][0] = ra;                                                   // x, y, conic a, b
             srec[lane][1] = make_float4(rb.x, pmin, rb.y, rb.w);                  // conic c, power floor, opacity, seg0
             srec[lane][2] = rc;                                                   // r, g, b, seg1
             srec[lane][3] = make_float4(rb.z, __uint_as_float(uslot), 0.f, 0.f);  // depth, record slot
-            __syncthreads();
+            wave_lds_sync();
+            uint64_t touched = 0;  // SPLIT: instances with a partial record from this wave
             while (todo) {
                 const int j = (int)__builtin_ctzll(todo);
                 todo &= todo - 1;
                 const uint32_t p = (uint32_t)(top - 1 - j);
                 const float4 q0 = srec[j][0], q1 = srec[j][1];
                 const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
-                float power[4], dys[4];
-                uint64_t act[4] = {act_all[0], act_all[1], act_all[2], act_all[3]};
+                float power[NS], dys[NS];
+                uint64_t act[NS];
+#pragma unroll
+                for (int k = 0; k < NS; ++k) act[k] = act_all[k];
                 if (vary) {
-    #pragma unroll
-                    for (int k = 0; k < 4; ++k) act[k] = __builtin_amdgcn_ballot_w64(p < lastc[k]);
+#pragma unroll
+                    for (int k = 0; k < NS; ++k) act[k] = __builtin_amdgcn_ballot_w64(p < lastc[k]);
                 }
-                uint64_t near[4];  // per strip: lanes whose pixel replays p and is within reach
+                uint64_t near[NS];  // per strip: lanes whose pixel replays p and is within reach
+                uint64_t any_near = 0;
                 const float dx = gx_ - pfx;
                 const float adxdx = ca * dx * dx, bdx = cb * dx;
-    #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
+#ifdef GSR_DEAD_SKIP
+                    if (!(active & (1u << k))) {  // idle strip in this batch
+                        near[k] = 0;
+                        power[k] = dys[k] = 0.f;
+                        continue;
+                    }
+#endif
                     const float dy = gy_ - pfy[k];
                     dys[k] = dy;
                     power[k] = __builtin_fmaf(-0.5f, adxdx + cc * dy * dy, -(bdx * dy));  // == -0.5 S - B
                     near[k] = act[k] & __builtin_amdgcn_ballot_w64(power[k] >= pm);
+                    any_near |= near[k];
                 }
                 STAT(0, 1);
-                if (!(near[0] | near[1] | near[2] | near[3])) {
+                if (!any_near) {
                     STAT(1, 1);
                     continue;
                 }
                 STAT(3, 1);
-                                const float4 q2 = srec[j][2], q3 = srec[j][3];
-                const float op = q1.z, dep = q3.x, s0 = q1.w;
-                const float c0 = q2.x, c1 = q2.y, c2 = q2.z, s1 = q2.w;
-                const uint32_t u = __float_as_uint(q3.y);
-                float* dst = contrib + (size_t)u * 12;
+                const float4 q2 = srec[j][2], q3 = srec[j][3];
+                const float op = q1.z, dep = q3.x, s0v = q1.w;
+                const float c0 = q2.x, c1 = q2.y, c2 = q2.z, s1v = q2.w;
                 float acc[12];
-    #pragma unroll
+#pragma unroll
                 for (int i = 0; i < 12; ++i) acc[i] = -0.0f;  // -0 + x == x: the first add folds away
                 // Strip k (rows 4k..4k+3) is replayed only if one of its pixels can pass.
-    #pragma unroll
-                for (int k = 0; k < 4; ++k) {
+#pragma unroll
+                for (int k = 0; k < NS; ++k) {
                     if (!near[k]) continue;
                     STAT(8, 1);
                     // near[k]: lanes replaying p (p < n_contrib) within reach (power >= the
@@ -616,8 +774,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                     float cdot = __builtin_fmaf(c0, dp0[k], da[k]);  // alpha channel (colour 1) first
                     cdot = __builtin_fmaf(c1, dp1[k], cdot);
                     cdot = __builtin_fmaf(c2, dp2[k], cdot);
-                    cdot = __builtin_fmaf(s0, ds0[k], cdot);
-                    cdot = __builtin_fmaf(s1, ds1[k], cdot);
+                    cdot = __builtin_fmaf(s0v, ds0[k], cdot);
+                    cdot = __builtin_fmaf(s1v, ds1[k], cdot);
                     cdot = __builtin_fmaf(dep, dd[k], cdot);
                     const float diff = cdot - Dk[k];
                     float dopa = diff * Tn;
@@ -644,7 +802,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                     T[k] = Tn;
                 }
 #ifdef GSR_MOMENT_MEAN
-                acc[7] = dx * acc[6];   // sum q dx   (dx is shared by the lane's 4 pixels)
+                acc[7] = dx * acc[6];   // sum q dx   (dx is shared by the lane's pixels)
                 acc[9] = dx * acc[7];   // sum q dx^2
                 acc[10] = dx * acc[8];  // sum q dx dy
 #else
@@ -654,7 +812,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                 // Qx, Qy combined after the reduction: for an elongated Gaussian a Qx and
                 // b Qy nearly cancel, which amplified the moments' rounding ~100x there.
                 {
-                    const float qx = dx * acc[6];  // sum q dx (dx is shared by the lane's 4 pixels)
+                    const float qx = dx * acc[6];  // sum q dx (dx is shared by the lane's pixels)
                     const float qy = acc[8];
                     acc[9] = dx * qx;              // sum q dx^2
                     acc[10] = dx * qy;             // sum q dx dy
@@ -665,10 +823,38 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
                 int vidx;
                 bool valid;
                 const float r = wave_reduce12(acc, lane, vidx, valid);
-                if (valid) dst[vidx] = r;
-                // Byte u marks slot u as written: one plain store of one byte by the whole
-                // wave (a uniform address; no atomic, no lane election).
-                written[u] = 1;
+                if constexpr (SPLIT) {
+                    if (valid) sh->part[wid][j][vidx] = r;
+                    touched |= 1ull << j;
+                } else {
+                    const uint32_t u = __float_as_uint(q3.y);
+                    if (valid) contrib[(size_t)u * 12 + vidx] = r;
+                    // Byte u marks slot u as written: one plain store of one byte by the whole
+                    // wave (a uniform address; no atomic, no lane election).
+                    written[u] = 1;
+                }
+            }
+            if constexpr (SPLIT) {
+                if (lane == 0) sh->tmask[wid] = touched;
+                __syncthreads();
+                // 128 threads: instance j = t / 2, channels 6 (t & 1) .. + 5; partials summed
+                // wave 0 + wave 1 (0 + x == x for a half that had none)
+                const int t = threadIdx.x, jj = t >> 1, h = t & 1;
+                const uint64_t m0 = sh->tmask[0], m1 = sh->tmask[1];
+                if (((m0 | m1) >> jj) & 1ull) {
+                    const bool w0 = (m0 >> jj) & 1ull, w1 = (m1 >> jj) & 1ull;
+                    const uint32_t u = __float_as_uint(sh->srec[0][jj][3].y);
+                    float v[6];
+#pragma unroll
+                    for (int c = 0; c < 6; ++c)
+                        v[c] = (w0 ? sh->part[0][jj][6 * h + c] : 0.f) + (w1 ? sh->part[1][jj][6 * h + c] : 0.f);
+                    float2* d = reinterpret_cast<float2*>(contrib + (size_t)u * 12 + 6 * h);
+                    d[0] = make_float2(v[0], v[1]);
+                    d[1] = make_float2(v[2], v[3]);
+                    d[2] = make_float2(v[4], v[5]);
+                    if (h == 0) written[u] = 1;
+                }
+                __syncthreads();  // the partials are read before the next batch overwrites them
             }
         }
     };
@@ -677,30 +863,117 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     else
         replay(std::false_type{});
     STAT_FLUSH(16)
-    WT_END(1, tile, n, top0)
+    WT_END(1, wslot, tile, n, top0, NS)
+}
+
+// The backward walks the forward's depth queue deepest first (TileSched): global work
+// index i -> bucket (a wave prefix over the 63 bucket counts, descending) -> tile.  Tiles
+// at least split_depth deep come first, one per block (top / bottom half on wave 0 / 1);
+// then two tiles per block, one per wave.  The grid is sized for no split (T / 2 ... T
+// blocks); blocks or waves past the queue return.  A tile's wave time grows with its
+// depth (the list positions it replays), so deepest-first is the longest-first order.
+__device__ __forceinline__ int queue_tile(const TileSched& ts, int T, uint32_t i, uint32_t pre, uint32_t cnt) {
+    // pre / cnt: this lane's bucket (63 - lane) exclusive prefix and count (lane 63: bucket 0, empty)
+    const uint64_t m = __builtin_amdgcn_ballot_w64(cnt > 0 && pre <= i);
+    if (!m) return -1;
+    const int L = 63 - __builtin_clzll(m);  // the last non-empty bucket starting at or before i
+    const uint32_t pL = __builtin_amdgcn_readlane(pre, L), cL = __builtin_amdgcn_readlane(cnt, L);
+    if (i >= pL + cL) return -1;
+    return __builtin_amdgcn_readfirstlane((int)ts.bq_list[(size_t)(63 - L) * T + (i - pL)]);
+}
+
+__global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k_render_bwd(
+    int W, int H, int gx, int T, int split_depth, uint32_t* __restrict__ sched,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ slot_vals,
+    const float4* __restrict__ rec, const float* __restrict__ bg, const float* __restrict__ alphas,
+    const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ dL_dsegs,
+    const float* __restrict__ dL_ddepths, const float* __restrict__ dL_dalphas, float* __restrict__ contrib,
+    uint8_t* __restrict__ written) {
+    __shared__ BwdShared sh;
+    const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const TileSched ts = tile_sched(sched - T, T);
+    // lane l: bucket 63 - l (deepest first); exclusive prefix over the lanes
+    const uint32_t cnt = lane < 63 ? ts.bq_cnt[63 - lane] : 0u;
+    uint32_t pre = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)pre, o, 64);
+        if (lane >= o) pre += y;
+    }
+    pre -= cnt;
+    // split tiles: buckets >= depth_bucket(split_depth), i.e. lanes <= 63 - that bucket
+    const int sb = split_depth > 0 ? (int)depth_bucket((uint32_t)split_depth) : 64;
+    const uint32_t Hs = sb < 64 ? (uint32_t)__builtin_amdgcn_readlane(pre + cnt, 63 - sb) : 0u;
+    const uint32_t b = blockIdx.x;
+    const bool split = b < Hs;  // block-uniform
+    const int tile = queue_tile(ts, T, split ? b : Hs + 2 * (b - Hs) + (uint32_t)wid, pre, cnt);
+    if (tile < 0) return;  // past the queue (a split block's waves share the tile: both return or neither)
+    if (split) {
+        bwd_tile<2, true>(W, H, gx, tile, 2 * wid, (int)(2 * b + wid), ranges, point_list, slot_vals, rec, bg,
+                          alphas, n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written,
+                          sh.srec[wid], &sh);
+    } else {
+        bwd_tile<4, false>(W, H, gx, tile, 0, (int)(2 * b + wid), ranges, point_list, slot_vals, rec, bg, alphas,
+                           n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, sh.srec[wid],
+                           nullptr);
+    }
+}
+
+// No split (split_bwd_depth = 0): one wave per block and tile, deepest first.
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_render_bwd1(
+    int W, int H, int gx, int T, uint32_t* __restrict__ sched,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ slot_vals,
+    const float4* __restrict__ rec, const float* __restrict__ bg, const float* __restrict__ alphas,
+    const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ dL_dsegs,
+    const float* __restrict__ dL_ddepths, const float* __restrict__ dL_dalphas, float* __restrict__ contrib,
+    uint8_t* __restrict__ written) {
+    __shared__ float4 srec[64][4];
+    const int lane = threadIdx.x & 63;
+    const TileSched ts = tile_sched(sched - T, T);
+    const uint32_t cnt = lane < 63 ? ts.bq_cnt[63 - lane] : 0u;
+    uint32_t pre = cnt;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)pre, o, 64);
+        if (lane >= o) pre += y;
+    }
+    pre -= cnt;
+    const int tile = queue_tile(ts, T, blockIdx.x, pre, cnt);
+    if (tile < 0) return;
+    bwd_tile<4, false>(W, H, gx, tile, 0, (int)blockIdx.x, ranges, point_list, slot_vals, rec, bg, alphas, n_contrib,
+                       dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, srec, nullptr);
 }
 
 }  // namespace
 
-void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
-                           const uint32_t* point_list, const float4* rec, const float* bg, float* out_color,
-                           float* out_depth, float* out_alpha, float* out_segment, uint32_t* n_contrib,
-                           hipStream_t st) {
+void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
+                           const uint2* ranges, const uint32_t* point_list, const float4* rec, const float* bg,
+                           float* out_color, float* out_depth, float* out_alpha, float* out_segment,
+                           uint32_t* n_contrib, hipStream_t st) {
     const int T = gx * gy;
     if (T == 0) return;
-    hipLaunchKernelGGL(k_render_fwd, dim3(T), dim3(64), 0, st, W, H, gx, order, ranges, point_list, rec, bg,
-                       out_color, out_depth, out_alpha, out_segment, n_contrib);
+    hipLaunchKernelGGL(k_render_fwd, dim3(2 * T), dim3(64), 0, st, W, H, gx, T, order, sched, ranges, point_list,
+                       rec, bg, out_color, out_depth, out_alpha, out_segment, n_contrib);
 }
 
-void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, const uint2* ranges,
-                            const uint32_t* point_list, const uint32_t* slot_vals, const float4* rec,
-                            const float* bg, const float* alpha, const uint32_t* n_contrib, const float* dL_dcolor,
-                            const float* dL_dsegment, const float* dL_ddepth, const float* dL_dalpha, float* contrib,
-                            uint8_t* written, hipStream_t st) {
+void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
+                            const uint2* ranges, const uint32_t* point_list, const uint32_t* slot_vals,
+                            const float4* rec, const float* bg, const float* alpha, const uint32_t* n_contrib,
+                            const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
+                            const float* dL_dalpha, float* contrib, uint8_t* written, hipStream_t st) {
     const int T = gx * gy;
     if (T == 0) return;
-    hipLaunchKernelGGL(k_render_bwd, dim3(T), dim3(64), 0, st, W, H, gx, order, ranges, point_list, slot_vals, rec,
-                       bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib, written);
+    (void)order;  // the backward follows the forward's depth queue
+    if (split_bwd_depth() <= 0) {
+        hipLaunchKernelGGL(k_render_bwd1, dim3(T), dim3(64), 0, st, W, H, gx, T, sched, ranges, point_list,
+                           slot_vals, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha,
+                           contrib, written);
+        return;
+    }
+    hipLaunchKernelGGL(k_render_bwd, dim3(T), dim3(128), 0, st, W, H, gx, T, split_bwd_depth(), sched, ranges,
+                       point_list,
+                       slot_vals, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib,
+                       written);
 }
 
 }  // namespace gsr

@@ -129,6 +129,7 @@ _DEBUG_FIELDS = {  # name -> (dtype, elements per unit, unit: P | I | T)
     "tiles_touched": (torch.int32, 1, "P"), "rec": (torch.float32, 16, "P"), "clamped": (torch.uint8, 1, "P"),
     "order": (torch.int32, 1, "P"), "goff": (torch.int32, 1, "P"), "point_list": (torch.int32, 1, "I"),
     "slot_vals": (torch.int32, 1, "I"), "ranges": (torch.int32, 2, "T"), "n_contrib_tiles": (torch.int32, 256, "T"),
+    "tile_order": (torch.int32, 1, "T+"),  # heavy-first tile order + the render schedule (gsr_internal.h TileSched)
 }
 
 
@@ -137,7 +138,7 @@ def debug_state(name, P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffe
     gsr_debug_copy in include/gsr.h).  Unsigned arrays are returned as int32."""
     dtype, per, unit = _DEBUG_FIELDS[name]
     T = ((W + 15) // 16) * ((H + 15) // 16)
-    n = {"P": P, "I": num_rendered, "T": T}[unit] * per
+    n = {"P": P, "I": num_rendered, "T": T, "T+": T + 4 + 64 + T + 64 * T}[unit] * per
     dev = geomBuffer.device
     out = torch.empty(max(n, 1), dtype=dtype, device=dev)
     ptr = lambda t: t.data_ptr() if t is not None and t.numel() else None
@@ -304,6 +305,13 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
 def set_option(name, value):
     """Process-wide tuning / test hook (include/gsr.h: gsr_set_option)."""
     _check(_lib.gsr_set_option(name.encode(), int(value)))
+
+
+# Tuning experiments without a rebuild: GSR_OPTIONS="name=value,name=value" is applied at
+# import (e.g. GSR_OPTIONS="split_fwd_bucket=10,split_bwd_bucket=0").
+for _kv in filter(None, os.environ.get("GSR_OPTIONS", "").split(",")):
+    _k, _v = _kv.split("=")
+    set_option(_k.strip(), int(_v))
 
 
 @functools.lru_cache(maxsize=64)

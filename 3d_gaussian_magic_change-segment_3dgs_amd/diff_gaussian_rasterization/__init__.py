@@ -235,7 +235,7 @@ class _RasterizeGaussians(torch.autograd.Function):
             grad_cov3Ds_precomp,
             None,
         )
-        return grads
+        return _finish_grads(ctx, grads)
 
 
 def rasterize_gaussians_multiview(means3D, means2D_list, sh, colors_precomp, segments, opacities, scales, rotations,
@@ -293,7 +293,25 @@ class _RasterizeGaussiansMultiview(torch.autograd.Function):
             _backward_views(views, means3D, colors_precomp, segments, scales, rotations, rs0.scale_modifier,
                             cov3Ds_precomp, sh, rs0.sh_degree, rs0.debug)
         ctx.views = None
-        return (g_means3D, g_sh, g_colors, g_segments, g_opacities, g_scales, g_rot, g_cov3D, None, *d2)
+        return _finish_grads(ctx, (g_means3D, g_sh, g_colors, g_segments, g_opacities, g_scales, g_rot, g_cov3D,
+                                   None, *d2))
+
+
+def _finish_grads(ctx, grads):
+    """Gradients handed to autograd: None where the input needs none (the backward's
+    zero placeholders for absent inputs are stride-0 views of one cached zero), and a
+    real zero tensor where an input that needs a gradient got such a placeholder, so that
+    hooks or in-place ops on .grad never see aliased memory (rasterize_points.cu:166-177
+    returns torch.zeros tensors)."""
+    out = []
+    for need, g in zip(ctx.needs_input_grad, grads):
+        if g is None or not need:
+            out.append(None)
+        elif g.numel() > 0 and 0 in g.stride():
+            out.append(torch.zeros(g.shape, dtype=g.dtype, device=g.device))
+        else:
+            out.append(g)
+    return tuple(out)
 
 
 class GaussianRasterizationSettings(NamedTuple):

@@ -29,16 +29,31 @@ def act_bwd_bytes(P, C=2):
     return P * 12 * (1 + 3 + 4 + C)
 
 
-def _events_ms(fn, reps):
+_SPREAD = {}
+
+
+def _events_ms(fn, reps, repeats=5):
+    """Median over `repeats` timings of `reps` back-to-back calls (ms per call); the
+    min / max of the repeats are kept in _SPREAD[fn] for the report."""
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     fn()
     torch.cuda.synchronize()
-    a.record()
-    for _ in range(reps):
-        fn()
-    b.record()
-    b.synchronize()
-    return a.elapsed_time(b) / reps
+    ts = []
+    for _ in range(repeats):
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) / reps)
+    ts.sort()
+    _SPREAD[fn] = (ts[0], ts[-1])
+    return ts[len(ts) // 2]
+
+
+def _spread(fn):
+    lo, hi = _SPREAD.get(fn, (None, None))
+    return {"min": round(lo, 4), "max": round(hi, 4), "repeats": 5} if lo is not None else None
 
 
 class _TrainArgs:
@@ -143,11 +158,12 @@ def measure(scene_cpu, cam_cpu, ups, device, reps=20, iters=10):
     # distCUDA2 (create_from_pcd) on the scene's means
     from gsr_train import distCUDA2
     pts = scene_cpu.means3D.to(device)
-    knn_ms = _events_ms(lambda: distCUDA2(pts), 3)
+    knn_ms = _events_ms(lambda: distCUDA2(pts), 3, repeats=3)
     ab = adam_bytes(P, M)
     return {
         "workload": f"P={P}, SH{deg}, 7 param groups (scene/gaussian_model.py:162-170)",
-        "adam_step": {"ms": round(adam_ms, 4), "algorithmic_bytes": ab,
+        "timing": "median of 5 repeats of back-to-back calls (hipEvents)",
+        "adam_step": {"ms": round(adam_ms, 4), "spread_ms": _spread(fused_adam), "algorithmic_bytes": ab,
                       "achieved_gbs": round(ab / (adam_ms * 1e-3) / 1e9, 1),
                       "frac": round(ab / (adam_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "bound": "hbm"},
         "activation_backward": {"ms": round(actbwd_ms, 4),
@@ -156,6 +172,7 @@ def measure(scene_cpu, cam_cpu, ups, device, reps=20, iters=10):
                             "note": "torch.optim.Adam (default foreach) + torch activations/cat and their "
                                     "autograd backward, same GPU"},
         "train_iteration_ms": {"fused": round(fused_iter_ms, 4), "reference_style": round(ref_iter_ms, 4),
+                               "fused_spread": _spread(fused_iter),
                                "note": "activations + rasterizer fwd+bwd (this library) + activation bwd + "
                                        "Adam step, one view"},
         "densify_and_prune": {"ms": round(densify_ms, 3), "P_before": P0, "P_after": m.num_points,

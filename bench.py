@@ -48,9 +48,28 @@ import torch  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X spec (MI355X_MICROARCH.md, chip-level parameters)
 SIMD_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
-# newest committed counter summary (tools/pmc.sh + tools/pmc_summary.py)
-PMC_SUMMARY = next((os.path.join(ROOT, "profiles", f) for f in ("round2_pmc_summary.json", "round1_pmc_summary.json")
+# newest committed counter summary (tools/pmc.sh + tools/pmc_summary.py); its counter-derived
+# fields are reported only when it was collected on the sources being benchmarked
+PMC_SUMMARY = next((os.path.join(ROOT, "profiles", f) for f in
+                    ("round3_pmc_summary.json", "round2_pmc_summary.json", "round1_pmc_summary.json")
                     if os.path.exists(os.path.join(ROOT, "profiles", f))), "")
+
+
+def pmc_for_this_build():
+    """(summary dict or None, provenance note)."""
+    if not PMC_SUMMARY:
+        return None, "no counter summary committed"
+    d = json.load(open(PMC_SUMMARY))
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        from pmc_summary import sources_sha256
+        cur = sources_sha256()
+    finally:
+        sys.path.pop(0)
+    name = os.path.relpath(PMC_SUMMARY, ROOT)
+    if d.get("sources_sha256") != cur:
+        return None, f"{name} was collected on other sources (counter fields omitted)"
+    return d, f"{name} (collected on these sources, sha256 {cur[:12]})"
 
 
 # {lib}: the collective library the process group actually runs on (dist.get_backend():
@@ -401,9 +420,10 @@ def main():
         avg_live = ms[dom_i] / cnt[dom_i]  # measured inside the timed region
         achieved = round(algorithmic_bytes(dom, P, I, HW, deg, B) / (avg_live * 1e-3) / 1e9, 1)
         traffic = cyc_per_valu = None
-        if PMC_SUMMARY:
+        pmc, pmc_note = pmc_for_this_build()
+        if pmc is not None:
             try:
-                pk = json.load(open(PMC_SUMMARY)).get("kernels", {}).get(dom, {})
+                pk = pmc.get("kernels", {}).get(dom, {})
                 traffic = pk.get("hbm_bytes_per_launch")
                 if pk.get("SQ_INSTS_VALU"):
                     # SIMD cycles per wave64 VALU instruction at the 2.4 GHz peak clock over the
@@ -420,8 +440,9 @@ def main():
                 "frac_of_measured_peak": round(achieved / measured_peak, 4) if measured_peak else None,
                 "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg, B),
                 "avg_launch_ms": round(avg_live, 4), "launches_timed": int(cnt[dom_i]),
-                "valu_instr_per_launch": (json.load(open(PMC_SUMMARY)).get("kernels", {}).get(dom, {}).get("SQ_INSTS_VALU")
-                                          if PMC_SUMMARY else None),
+                "valu_instr_per_launch": (pmc.get("kernels", {}).get(dom, {}).get("SQ_INSTS_VALU")
+                                          if pmc is not None else None),
+                "pmc_source": pmc_note,
                 "cycles_per_valu_instr": cyc_per_valu,
                 "whole_view_frac": round(view_bytes(P, I, HW, deg) * value / world / 1e9 / HBM_PEAK_GBS, 4)}
     out = {

@@ -153,7 +153,12 @@ GSR_API int gsr_forward(const gsr_settings* s, const gsr_inputs* in, void* geom,
 /* ---- backward.  Replaces Rasterizer::backward (rasterizer_impl.cu:348-458) /
  * RasterizeGaussiansBackwardCUDA (rasterize_points.cu:127-221).  dL_d* are the
  * upstream image gradients (same shapes as the forward outputs); alpha is the
- * forward's out_alpha; scratch has gsr_backward_scratch_bytes(num_rendered). */
+ * forward's out_alpha; scratch has gsr_backward_scratch_bytes(num_rendered).
+ * Contract: `in` must name the same colour source as the forward of this geom buffer
+ * (shs, or colors_precomp) with the same tensors.  The forward stores the SH direction
+ * Jacobian in geom only when it evaluated SH itself; a backward given shs after a
+ * forward with colors_precomp would read that field uninitialised.  (The reference
+ * recomputes it from shs; the Python layer always passes the forward's inputs.) */
 GSR_API int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, void* geom,
                  void* binning, void* img, int num_rendered, const float* alpha,
                  const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,

@@ -192,3 +192,34 @@ def test_stream_copy_reference_kernel(gpu_available):
     dst = torch.empty_like(src)
     assert _C._lib.gsr_stream_copy(src.data_ptr(), dst.data_ptr(), 12, 1, st) != 0  # not a multiple of 16
     assert _C._lib.gsr_stream_copy(src.data_ptr(), dst.data_ptr(), 16, 3, st) != 0  # bad variant
+
+
+def test_absent_input_gradients_are_not_aliased_views(gpu_available):
+    """the backward's zero placeholders for absent inputs (stride-0 views of one
+    cached zero) never reach autograd.  Inputs that need no gradient get None; a leaf whose
+    gradient is such a placeholder would get a real zero tensor, so in-place ops on .grad
+    work (the reference returns torch.zeros tensors, rasterize_points.cu:166-177)."""
+    import harness as Hn
+    from diff_gaussian_rasterization import _RasterizeGaussians
+    from gsr_tools.scene import synthetic_scene, orbit_camera
+    scene = synthetic_scene(2000, sh_degree=3, seed=71)
+    cam = orbit_camera(0, 96, 64, 80.0)
+    st = Hn.settings_for(cam, 3, "cuda")
+    L = lambda t: t.detach().cuda().clone().requires_grad_(True)
+    means3D, opac, segs = L(scene.means3D), L(scene.opacities), L(scene.segments)
+    cols = L(torch.rand(scene.P, 3))
+    g = torch.Generator().manual_seed(2)
+    A = torch.randn(scene.P, 3, 3, generator=g) * 0.02
+    S = A @ A.transpose(1, 2) + torch.eye(3) * 1e-5
+    cov = L(S[:, [0, 0, 0, 1, 1, 2], [0, 1, 2, 1, 2, 2]].contiguous())
+    m2 = torch.zeros_like(means3D, requires_grad=True)
+    E = torch.Tensor([])
+    out = _RasterizeGaussians.apply(means3D, m2, E, cols, segs, opac, E, E, cov, st)
+    fn = out[0].grad_fn
+    ups = [torch.randn_like(out[k]) for k in (0, 2, 3, 4)]
+    grads = fn.apply(ups[0], None, ups[1], ups[2], ups[3])  # the autograd node's backward
+    # inputs: means3D, means2D, sh, colors, segments, opacities, scales, rotations, cov3D, settings
+    assert grads[2] is None and grads[6] is None and grads[7] is None and grads[9] is None
+    for i in (0, 1, 3, 4, 5, 8):
+        assert grads[i] is not None and 0 not in grads[i].stride(), f"input {i}"
+        grads[i].add_(0.0)  # writable in place

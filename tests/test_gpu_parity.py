@@ -166,12 +166,43 @@ def test_everything_culled(gpu_available, oracle_mod):
         assert np.all(v == 0)
 
 
-def test_single_gaussian_tiny_image(gpu_available, oracle_mod):
-    scene = Scene(torch.tensor([[0.01, -0.02, 0.0]]), torch.rand(1, 16, 3) * 0.1, torch.tensor([[0.8]]),
-                  torch.tensor([[0.05, 0.08, 0.03]]), torch.tensor([[0.9, 0.1, 0.3, -0.2]]) / math.sqrt(0.95),
-                  torch.tensor([[0.3, 0.7]]), 3)
+@pytest.mark.parametrize("seed", [0, 165])
+def test_single_gaussian_tiny_image(gpu_available, oracle_mod, seed):
+    """One Gaussian over a 17x9 image (two tiles, one partly outside).  Each gradient
+    tensor is then ONE Gaussian's sum over ~150 pixels, and dopacity = sum_pixels
+    G dL_dalpha cancels: the scale-free bound becomes relative to a single cancelling sum.
+    A 300-seed sweep of the SH coefficients (tools/tiny_sweep.py, profiles/round3_tiny_sweep.txt)
+    puts the reference's own fp32 accumulation noise (oracle in fp32-atomic-order mode)
+    above 1e-5 of |dopacity| in 3 seeds (max 6.2e-5) and gsr in 17 (max 1.1e-4, seed 165:
+    the per-pixel dL_dalpha uses FMAs where the reference rounds each product, one ulp that
+    the cancellation amplifies).  So this case is held to max(1e-5 of the tensor maximum,
+    4x the reference's own fp32-order deviation); integer outputs and images stay exact /
+    1e-5.  (Before round 3 the SH draw was unseeded: the test passed or failed with the RNG
+    state left by earlier tests.)"""
+    g_ = torch.Generator().manual_seed(seed)
+    scene = Scene(torch.tensor([[0.01, -0.02, 0.0]]), torch.rand(1, 16, 3, generator=g_) * 0.1,
+                  torch.tensor([[0.8]]), torch.tensor([[0.05, 0.08, 0.03]]),
+                  torch.tensor([[0.9, 0.1, 0.3, -0.2]]) / math.sqrt(0.95), torch.tensor([[0.3, 0.7]]), 3)
     cam = make_camera(np.eye(3), np.array([0.0, 0.0, 2.0]), 17, 9, focal2fov(20.0, 17), focal2fov(20.0, 9))
-    compare(oracle_mod, scene, cam)
+    grads = Hn.upstream_grads(cam.height, cam.width)
+    g = Hn.run_gsr(scene, cam, grads=grads)
+    r = Hn.run_oracle(oracle_mod, scene, cam, grads=grads)
+    oracle_mod.set_acc32(True)
+    try:
+        r32 = Hn.run_oracle(oracle_mod, scene, cam, grads=grads)
+    finally:
+        oracle_mod.set_acc32(False)
+    assert_integer_parity(g, r)
+    assert_image_parity(g, r)
+    for k, ref in r["grads"].items():
+        if k not in g["grads"]:
+            continue
+        a = np.asarray(g["grads"][k], np.float64).reshape(ref.shape)
+        b, c = ref.astype(np.float64), r32["grads"][k].astype(np.float64)
+        if k == "dmeans2D":
+            a, b, c = a[:, :2], b[:, :2], c[:, :2]
+        bound = max(1e-5 * np.abs(b).max(), 4 * np.abs(c - b).max())
+        assert np.abs(a - b).max() <= bound, f"{k}: {np.abs(a - b).max():.3e} > {bound:.3e}"
 
 
 def test_deterministic(gpu_available, sh3_scene):
@@ -224,7 +255,7 @@ def test_grid_wider_than_packed_rect(gpu_available, oracle_mod):
     assert g["num_rendered"] > 1000
 
 
-@pytest.mark.parametrize("case", ["mt_small", "ragged", "big_gaussians"])
+@pytest.mark.parametrize("case", ["mt_small", "ragged", "big_gaussians", "tall_255_rows", "wide_255_cols"])
 def test_rows_binning_matches_radix_path(gpu_available, case):
     """binning_rows.hip (row-then-tile expansion, the default for grids <= 255 x 255
     tiles) and binning.hip's duplicate + radix tile sort build the same tile lists:
@@ -234,9 +265,16 @@ def test_rows_binning_matches_radix_path(gpu_available, case):
         scene, cam = synthetic_scene(60000, sh_degree=3, seed=41), orbit_camera(2, 640, 360, 400.0)
     elif case == "ragged":
         scene, cam = synthetic_scene(20000, sh_degree=3, seed=42), orbit_camera(5, 333, 250, 300.0)
-    else:
+    elif case == "big_gaussians":
         scene = synthetic_scene(3000, sh_degree=2, seed=43, log_scale=math.log(0.15), log_scale_std=0.6)
         cam = orbit_camera(1, 500, 300, 350.0)
+    else:
+        # grids at the 255-tile bound of the packed 8-bit rects: 16 x 255 tiles
+        # (the row level's LDS at gy = 255, lds_scan256 at n = 256) and 255 x 16 tiles, with
+        # Gaussians reaching the far edge (x1 or y1 = 255)
+        W, H = (256, 4080) if case == "tall_255_rows" else (4080, 256)
+        scene = synthetic_scene(40000, sh_degree=1, seed=44, extent=2.5, log_scale=math.log(0.03))
+        cam = make_camera(np.eye(3), np.array([0.0, 0.0, 4.0]), W, H, focal2fov(1700.0, W), focal2fov(1700.0, H))
     grads = Hn.upstream_grads(cam.height, cam.width)
     out = {}
     try:
@@ -249,7 +287,75 @@ def test_rows_binning_matches_radix_path(gpu_available, case):
         _C.set_option("rows_binning", 1)
     (a, ga), (b, gb) = out[1], out[0]
     assert a["num_rendered"] == b["num_rendered"] > 0
-    for k in ("point_list", "ranges", "n_contrib", "color", "depth", "alpha", "segment", "radii"):
+    if case.endswith("255_rows") or case.endswith("255_cols"):
+        gx, gy = (cam.width + 15) // 16, (cam.height + 15) // 16
+        assert max(gx, gy) == 255
+        rg = a["ranges"].reshape(gy, gx, 2)
+        edge = rg[-1, :, :] if gy == 255 else rg[:, -1, :]
+        assert int((edge[..., 1] > edge[..., 0]).sum()) > 0, "no Gaussian reaches the 255th tile row / column"
+    for k in ("point_list", "slot_vals", "ranges", "n_contrib", "color", "depth", "alpha", "segment", "radii"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    vis = a["radii"] > 0  # the row path writes goff for visible Gaussians only
+    np.testing.assert_array_equal(a["goff"][vis], b["goff"][vis], err_msg="goff")
     for k in ga:
         np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
+
+
+def _tile_queue(state, T):
+    """The render schedule after the T-entry tile order (gsr_internal.h TileSched)."""
+    t = state["tile_order"].astype(np.int64)
+    sched = t[T:T + 4]
+    cnt = t[T + 4:T + 68]
+    lst = t[T + 68 + T:].reshape(64, T)
+    return sched, cnt, lst
+
+
+@pytest.mark.parametrize("split,rows", [((1, 1), 1), ((1, 0), 1), ((0, 1), 1), ((1, 1), 0), ((10, 256), 1)])
+def test_split_tiles(gpu_available, oracle_mod, split, rows):
+    """Long tiles get two waves.  Forward: tiles whose list length has bit length >= B
+    (n >= 2^(B-1)) are rendered as top / bottom halves (pixel results bit-identical to the
+    one-wave tile).  Backward: it walks the forward's depth queue deepest first, and tiles
+    whose deepest contributor is at least D deep get a block of two waves, each reducing a
+    partial record per instance, summed wave 0 + wave 1.  (B, D) = (1, 1) splits every
+    non-empty tile; forced on a small scene, for the row-binning and the radix
+    (k_tile_order) schedules.  Checked: the split count, that the queue files every tile
+    with a contributor exactly once under its depth bucket, bit-identical forward outputs,
+    parity of everything with the oracle."""
+    from diff_gaussian_rasterization import _C
+    scene, cam = synthetic_scene(60000, sh_degree=3, seed=41), orbit_camera(2, 640, 360, 400.0)
+    grads = Hn.upstream_grads(cam.height, cam.width)
+    out = {}
+    try:
+        _C.set_option("rows_binning", rows)
+        for mode in ("split", "none"):
+            bf, bd = split if mode == "split" else (0, 0)
+            _C.set_option("split_fwd_bucket", bf)
+            _C.set_option("split_bwd_depth", bd)
+            out[mode] = Hn.run_gsr(scene, cam, grads=grads)
+    finally:
+        _C.set_option("rows_binning", 1)
+        _C.set_option("split_fwd_bucket", 0)
+        _C.set_option("split_bwd_depth", 0)
+    a, b = out["split"], out["none"]
+    T = ((cam.width + 15) // 16) * ((cam.height + 15) // 16)
+    rg = b["ranges"].reshape(-1, 2).astype(np.int64)
+    lens = rg[:, 1] - rg[:, 0]
+    sched, cnt, lst = _tile_queue(a, T)
+    assert sched[0] == (0 if split[0] == 0 else int((lens >= (1 << (split[0] - 1))).sum())), "forward split count"
+    assert _tile_queue(b, T)[0][0] == 0
+    # the queue: every tile with a contributor once, under ceil(depth / 16) (capped at 63)
+    depth = a["n_contrib_tiles"].reshape(T, 256).max(1).astype(np.int64)
+    bucket = np.minimum((depth + 15) // 16, 63)
+    filed = np.concatenate([lst[k, :cnt[k]] for k in range(64)])
+    assert cnt[0] == 0 and len(filed) == int((depth > 0).sum()) == len(set(filed.tolist()))
+    for k in range(1, 64):
+        assert np.all(bucket[lst[k, :cnt[k]]] == k), f"bucket {k}"
+    for k in ("n_contrib", "color", "depth", "alpha", "segment", "radii"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    r = Hn.run_oracle(oracle_mod, scene, cam, grads=grads)
+    r.pop("_run", None)
+    assert_integer_parity(a, r)
+    assert_grad_parity(a["grads"], r["grads"])
+    if split[1] == 0:  # backward unsplit: gradients bit-identical
+        for k in a["grads"]:
+            np.testing.assert_array_equal(a["grads"][k], b["grads"][k], err_msg=k)

@@ -29,8 +29,22 @@ def load(sub):
     return acc
 
 
+def sources_sha256():
+    """Hash of the HIP sources the counters were collected on (bench.py compares it with
+    the build it times before reporting the counter-derived fields)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd", "csrc")
+    for f in sorted(os.listdir(csrc)):
+        if f.endswith((".hip", ".h")) and not f.startswith("."):
+            h.update(f.encode())
+            h.update(open(os.path.join(csrc, f), "rb").read())
+    h.update(open(os.path.join(ROOT, "include", "gsr.h"), "rb").read())
+    return h.hexdigest()
+
+
 def main():
-    out = {"note": __doc__.strip(), "kernels": {}}
+    out = {"note": __doc__.strip(), "sources_sha256": sources_sha256(), "kernels": {}}
     merged = defaultdict(dict)
     for sub in ("fetch", "write", "sq"):
         for k, cs in load(sub).items():

@@ -19,8 +19,7 @@ import harness as Hn  # noqa: E402
 from gsr_tools.scene import config_scene_and_camera  # noqa: E402
 
 
-def analyse(name, tr, ntiles, slots):
-    tr = tr[:ntiles]
+def analyse(name, tr, slots):
     t0, t1 = tr[:, 0].astype(np.int64), tr[:, 1].astype(np.int64)
     ok = (t1 > 0) & (t0 > 0)
     tr, t0, t1 = tr[ok], t0[ok], t1[ok]
@@ -29,6 +28,7 @@ def analyse(name, tr, ntiles, slots):
     span = e.max()
     dur = e - s
     n = (tr[:, 2] >> 32).astype(np.int64)
+    mode = ((tr[:, 2] >> 24) & 255).astype(np.int64)
     depth = (tr[:, 3] & 0xFFFFFF).astype(np.int64)
     xcc = ((tr[:, 3] >> 24) & 15).astype(np.int64)
     print(f"== {name}: {len(tr)} waves, span {span / 1e3:.1f} us, wave duration mean {dur.mean() / 1e3:.1f} us, "
@@ -52,7 +52,11 @@ def analyse(name, tr, ntiles, slots):
         print(f"   duration ~ {c[0]:.1f} ns x depth + {c[1] / 1e3:.2f} us; depth mean {depth.mean():.0f} "
               f"max {depth.max()}, list n mean {n.mean():.0f} max {n.max()}")
     print("   waves per XCC:", np.bincount(xcc, minlength=8).tolist())
-    return dict(start=s, end=e, depth=depth, n=n, xcc=xcc)
+    for m in sorted(set(mode.tolist())):
+        sel = mode == m
+        print(f"   mode {m} (quadrants/strips per wave): {sel.sum()} waves, duration mean {dur[sel].mean() / 1e3:.1f} us "
+              f"max {dur[sel].max() / 1e3:.1f} us, depth mean {depth[sel].mean():.0f}")
+    return dict(start=s, end=e, depth=depth, n=n, xcc=xcc, mode=mode)
 
 
 def main():
@@ -60,20 +64,22 @@ def main():
     out = sys.argv[2] if len(sys.argv) > 2 else None
     from diff_gaussian_rasterization import _C
     lib = _C._lib
-    lib.gsr_wave_trace_read.argtypes = [ctypes.c_void_p]
+    lib.gsr_wave_trace_read.argtypes = [ctypes.c_void_p, ctypes.c_int]
     scene, cam = config_scene_and_camera(cfg)
     grads = Hn.upstream_grads(cam.height, cam.width)
-    for _ in range(4):
+    buf = np.zeros((2, 32768, 4), np.uint64)
+    for _ in range(3):
         Hn.run_gsr(scene, cam, grads=grads, want_state=False)
     torch.cuda.synchronize()
-    buf = np.zeros((2, 32768, 4), np.uint64)
-    assert lib.gsr_wave_trace_read(buf.ctypes.data) == 0
-    ntiles = ((cam.width + 15) // 16) * ((cam.height + 15) // 16)
+    assert lib.gsr_wave_trace_read(buf.ctypes.data, 1) == 0  # clear
+    Hn.run_gsr(scene, cam, grads=grads, want_state=False)
+    torch.cuda.synchronize()
+    assert lib.gsr_wave_trace_read(buf.ctypes.data, 0) == 0
     props = torch.cuda.get_device_properties(0)
     slots = props.multi_processor_count * 4 * 4  # 4 SIMDs per CU x 4 waves per SIMD (the kernels' cap)
     res = {}
     for k, name in enumerate(("k_render_fwd", "k_render_bwd")):
-        r = analyse(name, buf[k], ntiles, slots if k == 1 else props.multi_processor_count * 4 * 5)
+        r = analyse(name, buf[k], slots if k == 1 else props.multi_processor_count * 4 * 5)
         res.update({f"{name}_{a}": v for a, v in r.items()})
     if out:
         np.savez_compressed(out, **res)
