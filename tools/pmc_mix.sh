@@ -22,7 +22,7 @@ for f in glob.glob(sys.argv[1] + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
         m = re.search(r"(k_[A-Za-z0-9_]+)", r.get("Kernel_Name", ""))
         if m: acc[m.group(1)][r["Counter_Name"]].append(float(r["Counter_Value"]))
-for k in ("k_render_bwd", "k_render_fwd", "k_gaussian_backward", "k_tiles_scatter", "k_preprocess", "k_rows_scatter", "k_radix_scatter"):
+for k in ("k_render_bwd", "k_render_bwd1", "k_render_fwd", "k_gaussian_backward", "k_tiles_scatter", "k_preprocess", "k_rows_scatter", "k_radix_scatter"):
     if k in acc:
         print(k, {c: round(sum(v) / len(v) / 1e6, 2) for c, v in sorted(acc[k].items())})
 PY
