@@ -229,6 +229,12 @@ def main():
                          "(all-gather of 3-float dRGB rows + all-reduce of 13 floats, gsr_tools.dp.ShExchange); "
                          "auto = the one with fewer bytes per link for the step's views per rank")
     args = ap.parse_args()
+    # The bench line is the only thing on stdout: native libraries (RCCL prints its version
+    # banner at communicator set-up) write to file descriptor 1 directly, so fd 1 is pointed
+    # at stderr for the run and the JSON line goes to the saved descriptor.
+    sys.stdout.flush()
+    json_fd = os.dup(1)
+    os.dup2(2, 1)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -242,7 +248,9 @@ def main():
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
     dist = None
-    if world > 1:
+    # GSR_DIST_FORCE=1 (under torch.distributed.run): a process group even at world size 1,
+    # so a one-GPU box runs the exchange through RCCL exactly as the N-GPU bench issues it
+    if world > 1 or os.environ.get("GSR_DIST_FORCE") == "1":
         import torch.distributed as dist
         backend = os.environ.get("GSR_DIST_BACKEND", "nccl")  # nccl == RCCL over xGMI on ROCm
         if backend == "nccl":
@@ -462,7 +470,7 @@ def main():
                    "parallelism": f"dp{world}" + ((" (views sharded; " +
                                                    EXCHANGE_DESC[step.exchange].format(lib=dinfo["collective_lib"]) +
                                                    " per step, overlapped with the next step's render)")
-                                                  if world > 1 else ""),
+                                                  if dist is not None else ""),
                    "dist_backend": dinfo["backend"], "world_size": dinfo["world_size"],
                    "rccl_version": dinfo["rccl_version"]},
         "roofline": roof,
@@ -496,7 +504,8 @@ def main():
         if args.stages:
             for k, v in stages.items():
                 print(f"{k:14s} {v['ms_per_step']:8.4f} ms/step  {v['gbs']:8.1f} GB/s", file=sys.stderr)
-        print(json.dumps(out), flush=True)
+        sys.stdout.flush()
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
         dist.destroy_process_group()
 

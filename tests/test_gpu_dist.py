@@ -1,9 +1,11 @@
-"""The multi-GPU path end to end with the real HIP kernels: two spawned ranks (gloo,
-both on cuda:0 -- this pool gives a test one GPU; bench.py --gpus N runs the same
-helpers over RCCL), each rendering its own view of the replicated scene through the
-drop-in GaussianRasterizer and running libgsr's backward.  The exchanged gradients
-must equal the sum of the two single-view gradients (computed on each rank with the
-same library, no exchange):
+"""The multi-GPU path end to end with the real HIP kernels: spawned ranks, each rendering
+its own view of the replicated scene through the drop-in GaussianRasterizer and running
+libgsr's backward.  Two cases: two gloo ranks sharing cuda:0 (this pool gives a test one
+GPU), and one RCCL rank ("nccl" backend, world size 1 -- RCCL refuses two ranks on one
+device; the collectives, all_gather_into_tensor and the side-stream waits of the exchange
+still run through RCCL on the GPU, as bench.py --gpus N issues them).  The exchanged
+gradients must equal the sum of the ranks' single-view gradients (computed on each rank
+with the same library, no exchange):
 
   * dp.allreduce_bucket(dp.arena_of(g)) -- the bucket all-reduce bench.py issues:
     bit-exact (a two-term fp32 sum is the same either way);
@@ -31,14 +33,14 @@ P_TEST = 6000
 NAMES = ("means3D", "shs", "opacities", "scales", "rotations", "segments")
 
 
-def _setup():
+def _setup(world):
     import sys
     sys.path[:0] = [ROOT, os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd"), os.path.join(ROOT, "tests")]
     import harness as Hn
     from gsr_tools.scene import synthetic_scene, orbit_camera
     scene = synthetic_scene(P_TEST, sh_degree=3, seed=61)
     views = []
-    for v in range(2):
+    for v in range(max(world, 2)):
         cam = orbit_camera(v, 160, 120, 150.0, n_views=4)
         views.append((Hn.settings_for(cam, 3, "cuda"), {k: t.cuda() for k, t in Hn.upstream_grads(120, 160, seed=20 + v).items()}))
     leaves = {k: getattr(scene, k).detach().cuda().clone().requires_grad_(True) for k in NAMES}
@@ -63,20 +65,21 @@ def _grad(leaves, view):
     return g
 
 
-def _worker(rank, world, port, out_q):
+def _worker(rank, world, port, backend, out_q):
     import torch.distributed as dist
     try:
         torch.cuda.set_device(0)
-        leaves, views = _setup()
+        leaves, views = _setup(world)
         from diff_gaussian_rasterization import defer_sh_gradients
         from gsr_tools import dp
-        dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+        kw = {"device_id": torch.device("cuda", 0)} if backend == "nccl" else {}
+        dist.init_process_group(backend, init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world, **kw)
         P, M = P_TEST, leaves["shs"].shape[1]
-        # reference: the two single-view drop-in gradients, summed here (no exchange)
-        g0, g1 = _grad(leaves, views[0]), _grad(leaves, views[1])
-        ref = {k: (a + b) for k, a, b in zip(NAMES, g0, g1)}
-        ref_m2 = (g0, g1)[rank][-1]
-        res = {}
+        # reference: the ranks' single-view drop-in gradients, summed here (no exchange)
+        gs = [_grad(leaves, views[v]) for v in range(world)]
+        ref = {k: sum(g[i] for g in gs) for i, k in enumerate(NAMES)}
+        ref_m2 = gs[rank][-1]
+        res = {"backend": str(dist.get_backend())}
 
         # 1. bucket all-reduce over the backward's gradient arena
         g = _grad(leaves, views[rank])
@@ -137,15 +140,16 @@ def _free_port():
     return p
 
 
-def test_two_ranks_real_backward_exchange(gpu_available):
+@pytest.mark.parametrize("backend,world", [("gloo", 2), ("nccl", 1)])
+def test_ranks_real_backward_exchange(gpu_available, backend, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, backend, q)) for r in range(world)]
     for p in procs:
         p.start()
     try:
-        res = [q.get(timeout=240) for _ in range(2)]
+        res = [q.get(timeout=240) for _ in range(world)]
     finally:
         for p in procs:
             p.join(timeout=60)
@@ -154,6 +158,7 @@ def test_two_ranks_real_backward_exchange(gpu_available):
     for rank, r, err in res:
         assert err is None, f"rank {rank} failed:\n{err}"
     for rank, r, _ in res:
+        assert r["backend"] == backend
         for k, e in r["allreduce"].items():
             assert e == 0.0, f"rank {rank} allreduce {k}: max |diff| {e:.3e}"
         for mode in ("sh_grad", "sh_backward"):
