@@ -31,6 +31,7 @@ def analyse(name, tr, slots):
     mode = ((tr[:, 2] >> 24) & 255).astype(np.int64)
     depth = (tr[:, 3] & 0xFFFFFF).astype(np.int64)
     xcc = ((tr[:, 3] >> 24) & 15).astype(np.int64)
+    hwid = (tr[:, 3] >> 32).astype(np.int64)  # HW_ID: wave[3:0] simd[5:4] cu[11:8] sh[12] se[15:13]
     print(f"== {name}: {len(tr)} waves, span {span / 1e3:.1f} us, wave duration mean {dur.mean() / 1e3:.1f} us, "
           f"max {dur.max() / 1e3:.1f} us, p50 {np.median(dur) / 1e3:.1f}, p90 {np.percentile(dur, 90) / 1e3:.1f}")
     bins = np.arange(0, span + 1000, 1000)
@@ -56,7 +57,15 @@ def analyse(name, tr, slots):
         sel = mode == m
         print(f"   mode {m} (quadrants/strips per wave): {sel.sum()} waves, duration mean {dur[sel].mean() / 1e3:.1f} us "
               f"max {dur[sel].max() / 1e3:.1f} us, depth mean {depth[sel].mean():.0f}")
-    return dict(start=s, end=e, depth=depth, n=n, xcc=xcc, mode=mode)
+    simd = xcc * 4096 + ((hwid >> 13) & 7) * 512 + ((hwid >> 12) & 1) * 256 + ((hwid >> 8) & 15) * 4 + ((hwid >> 4) & 3)
+    ends = {}
+    for u, t1 in zip(simd.tolist(), e.tolist()):
+        ends[u] = max(ends.get(u, 0), t1)
+    work = np.bincount(np.unique(simd, return_inverse=True)[1], weights=dur.astype(np.float64))
+    print(f"   SIMDs used {len(ends)}; per-SIMD last end: min {min(ends.values()) / 1e3:.1f} "
+          f"median {np.median(list(ends.values())) / 1e3:.1f} max {max(ends.values()) / 1e3:.1f} us; "
+          f"per-SIMD sum of wave durations: median {np.median(work) / 1e3:.0f} max {work.max() / 1e3:.0f} us")
+    return dict(start=s, end=e, depth=depth, n=n, xcc=xcc, mode=mode, hwid=hwid, simd=simd)
 
 
 def main():
