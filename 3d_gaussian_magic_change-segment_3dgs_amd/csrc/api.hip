@@ -234,11 +234,11 @@ int gsr_set_option(const char* name, long long value) {
         return 0;
     }
     if (std::string(name) == "split_fwd_bucket") {  // render forward: tiles with n >= 2^(v-1) on two waves; 0 = off
-        gsr::set_split_buckets((int)value, -1);
+        gsr::set_split_buckets((int)value, gsr::split_bwd_depth());
         return 0;
     }
     if (std::string(name) == "split_bwd_depth") {  // render backward: tiles this deep on two waves; 0 = off
-        gsr::set_split_buckets(-1, (int)value);
+        gsr::set_split_buckets(gsr::split_fwd_bucket(), (int)value);
         return 0;
     }
     if (std::string(name) == "sort_lookback_max") {

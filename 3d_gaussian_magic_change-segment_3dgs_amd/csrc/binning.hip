@@ -812,20 +812,27 @@ void launch_scan_exclusive(const uint32_t* src, uint32_t* out, size_t n, const u
                        W.status, W.counter, nullptr, 0, n_dev);
 }
 
-// Split buckets (gsr_set_option "split_fwd_bucket" / "split_bwd_bucket"): tiles whose
-// list length has at least this bit length (n >= 2^(B-1)) get two waves.
+// Split buckets (gsr_set_option "split_fwd_bucket" / "split_bwd_depth"; a negative value
+// restores the default): tiles whose list length has at least this bit length
+// (n >= 2^(B-1)) get two waves.  Forward default B = 8 (n >= 128: at the metric scene every
+// tile that goes deeper than a few dozen positions): a SIMD serves its waves oldest first and
+// ends when its tiles' total work is done, so the ~5300 deep tiles dealt over 1024 SIMDs x 5
+// wave slots left the most loaded SIMD 25% behind the median (profiles/round3_wave_trace_simd.txt);
+// twice as many half-size units even that out: render_fwd 0.227 -> 0.204 ms
+// (profiles/round3_split_sweep.txt: B = 7 0.203-0.205, 9 0.207-0.213, 1 0.206, 10-12 slower).
 #ifndef GSR_SPLIT_FWD
-#define GSR_SPLIT_FWD 0
+#define GSR_SPLIT_FWD 8
 #endif
 #ifndef GSR_SPLIT_BWD_DEPTH
 #define GSR_SPLIT_BWD_DEPTH 0
 #endif
 static int g_split_fwd = GSR_SPLIT_FWD, g_split_bwd_depth = GSR_SPLIT_BWD_DEPTH;
 void set_split_buckets(int fwd_bucket, int bwd_depth) {
-    if (fwd_bucket >= 0) g_split_fwd = fwd_bucket;
-    if (bwd_depth >= 0) g_split_bwd_depth = bwd_depth;
+    g_split_fwd = fwd_bucket >= 0 ? fwd_bucket : GSR_SPLIT_FWD;
+    g_split_bwd_depth = bwd_depth >= 0 ? bwd_depth : GSR_SPLIT_BWD_DEPTH;
 }
 int split_bwd_depth() { return g_split_bwd_depth; }
+int split_fwd_bucket() { return g_split_fwd; }
 
 void launch_tile_order_counted(const uint2* ranges, int T, uint32_t* bucket_words, uint32_t* order,
                                hipStream_t st) {

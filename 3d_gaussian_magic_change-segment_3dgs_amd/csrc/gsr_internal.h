@@ -289,8 +289,9 @@ void set_sort_lookback_max(size_t n);
 // length buckets >= the forward's split bucket (set_split_buckets; 0 = no split), and zero
 // the backward queue's counters (TileSched).  bwd_depth: the backward splits tiles whose
 // deepest contributor is at least this deep (0 = no split; a render.hip launch argument).
-void set_split_buckets(int fwd_bucket, int bwd_depth);
+void set_split_buckets(int fwd_bucket, int bwd_depth);  // negative: the built-in default
 int split_bwd_depth();
+int split_fwd_bucket();
 void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st);
 // the same from bucket counts already taken (row binning): many blocks, no serial pass
 void launch_tile_order_counted(const uint2* ranges, int T, uint32_t* bucket_words, uint32_t* order, hipStream_t st);

@@ -334,8 +334,8 @@ def test_split_tiles(gpu_available, oracle_mod, split, rows):
             out[mode] = Hn.run_gsr(scene, cam, grads=grads)
     finally:
         _C.set_option("rows_binning", 1)
-        _C.set_option("split_fwd_bucket", 0)
-        _C.set_option("split_bwd_depth", 0)
+        _C.set_option("split_fwd_bucket", -1)  # the defaults
+        _C.set_option("split_bwd_depth", -1)
     a, b = out["split"], out["none"]
     T = ((cam.width + 15) // 16) * ((cam.height + 15) // 16)
     rg = b["ranges"].reshape(-1, 2).astype(np.int64)
