@@ -348,12 +348,12 @@ def main():
 
     def timed(fn, k, per_step=None):
         """k steps between a barrier + device sync on both sides; max over ranks.  Python's
-        cyclic GC is paused inside (collected just before): a collection pass in the
-        middle of the loop stalls the host for milliseconds, which leaves the GPU idle
-        behind the per-view num_rendered sync.  per_step (a list) receives each step's
-        duration from events recorded on the compute stream between the steps."""
+        cyclic GC is paused (collected before the untimed stage pass that precedes this, not
+        here: a collection while the GPU sits idle before the timed region let the clocks
+        drop, and the first five timed steps ran 10-28% slow; a collection inside the loop
+        stalls the host behind the per-view num_rendered sync).  per_step (a list) receives
+        each step's duration from events recorded on the compute stream between the steps."""
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(k + 1)] if per_step is not None else None
-        gc.collect()
         gc.disable()
         if dist is not None:
             dist.barrier()
@@ -394,6 +394,8 @@ def main():
         return ms, cnt
 
     collect()  # drop anything pending
+    gc.collect()  # before the stage pass, so the GPU is busy right up to the timed region
+    gc.disable()
     # Stage pass (untimed): every stage bracketed by events -> the stage table and the
     # dominant stage.  The brackets cost a few microseconds each, so the timed region
     # below records events around the dominant stage only.
@@ -460,6 +462,9 @@ def main():
         "step_ms": ({"mean": round(sum(step_ms) / len(step_ms), 4),
                      "median": round(sorted(step_ms)[len(step_ms) // 2], 4),
                      "p90": round(sorted(step_ms)[min(len(step_ms) - 1, int(0.9 * len(step_ms)))], 4),
+                     "max": round(max(step_ms), 4),
+                     "slowest": [(i, round(t, 3)) for t, i in sorted(((t, i) for i, t in enumerate(step_ms)),
+                                                                    reverse=True)[:5]],
                      "source": "hipEvents between steps on the compute stream (rank 0)"} if step_ms else None),
         "vs_baseline": None, "dtype": "f32", "data": "synthetic (SURVEY.md s8d generator, seed 0; upstream grads "
                                                     "N(0,1)*1e-3 seed 1)",
