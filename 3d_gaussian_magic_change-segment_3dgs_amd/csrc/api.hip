@@ -241,6 +241,10 @@ int gsr_set_option(const char* name, long long value) {
         gsr::set_split_buckets(gsr::split_fwd_bucket(), (int)value);
         return 0;
     }
+    if (std::string(name) == "sort_grouped") {  // depth sort: grouped look-back passes (default on)
+        gsr::set_sort_grouped(value != 0);
+        return 0;
+    }
     if (std::string(name) == "sort_lookback_max") {
         gsr::set_sort_lookback_max(value < 0 ? 0 : (size_t)value);
         return 0;

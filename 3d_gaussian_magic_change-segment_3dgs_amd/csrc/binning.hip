@@ -15,6 +15,25 @@
 //      ceil((32+log2 T)/8) passes over 64-bit keys.
 #include "gsr_internal.h"
 
+#ifdef GSR_SORT_TRACE
+// Timeline build (tools/sort_trace.py): per tile of each look-back radix pass (slot = shift /
+// 8), s_memrealtime (100 MHz) at entry, after the tile index, after the ranking barrier, after
+// the look-back barrier and at the end, plus the XCC id.
+__device__ unsigned long long g_gsr_strace[5][1024][6];  // [4]: k_radix_hist blocks
+extern "C" __attribute__((visibility("default"))) int gsr_sort_trace_read(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gsr_strace), sizeof(g_gsr_strace)) != hipSuccess) return -1;
+    if (reset) {
+        void* d = nullptr;
+        if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_gsr_strace)) != hipSuccess) return -1;
+        if (hipMemset(d, 0, sizeof(g_gsr_strace)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#define ST_T(var) const unsigned long long var = __builtin_amdgcn_s_memrealtime();
+#else
+#define ST_T(var)
+#endif
+
 namespace gsr {
 
 namespace {
@@ -255,6 +274,7 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
                                                              int passes, int per_pass, int key_bits,
                                                              uint32_t* __restrict__ hist, uint32_t* span,
                                                              int skip_sentinel, const uint32_t* n_dev) {
+    ST_T(st0)
     if (n_dev) n = min(n, (size_t)*n_dev);
     __shared__ uint32_t cnt[4][RADIX];
     __shared__ uint32_t s_span[8];
@@ -273,6 +293,10 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
         const size_t idx = base + (size_t)i * HIST_THREADS;
         kk[i] = idx < n ? keys[idx] : 0u;
     }
+#ifdef GSR_SORT_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ST_T(st1)
+#endif
 #pragma unroll
     for (int i = 0; i < HIST_ITEMS; ++i) {
         const size_t idx = base + (size_t)i * HIST_THREADS;
@@ -313,10 +337,19 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
         }
     }
     __syncthreads();
+    ST_T(st2)
     if (threadIdx.x < RADIX)
         for (int p = 0; p < passes; ++p)
             if (cnt[p][threadIdx.x]) atomicAdd(&hist[p * RADIX + threadIdx.x], cnt[p][threadIdx.x]);
     if (threadIdx.x < 2 * passes && s_span[threadIdx.x]) atomicMax(&span[threadIdx.x], s_span[threadIdx.x]);
+#ifdef GSR_SORT_TRACE
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < 1024) {
+        unsigned long long* w = g_gsr_strace[4][blockIdx.x];
+        w[0] = st0; w[1] = st0; w[2] = st1; w[3] = st2; w[4] = __builtin_amdgcn_s_memrealtime();
+        w[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 15u;
+    }
+#endif
 }
 
 // Per-tile digit histogram -> hist[digit * ntiles + tile] (table-driven passes).  One
@@ -375,6 +408,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
     uint64_t* status, uint32_t* counter, const uint32_t* __restrict__ vals2_in, uint32_t* __restrict__ vals2_out,
     SortFinal fin, const uint32_t* span, const uint32_t* n_dev) {
     constexpr int NT = 64 * WAVES, TILE = NT * ITEMS;
+    ST_T(st0)
     if (n_dev) n = min(n, (size_t)*n_dev);
     for (size_t i = (size_t)blockIdx.x * NT + threadIdx.x; i < fin.zero16; i += (size_t)gridDim.x * NT)
         fin.zero[i] = make_uint4(0u, 0u, 0u, 0u);
@@ -387,6 +421,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
     // span = this pass's digit range over the keys that matter (k_radix_hist)
     const uint32_t sp_lo = LB && span ? span[0] : 0u, sp_hi = LB && span ? span[1] : 1u;
     const int t = LB ? lb_tile_index(counter) : (int)blockIdx.x;
+    ST_T(st1)
     if (LB && span && (sp_lo == 0u || 256u - sp_lo == sp_hi - 1u)) {
         // Every key that matters has the same digit in this pass: a stable pass is the
         // identity on them, so the tile is copied through and the look-back chain is
@@ -402,6 +437,14 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
                 if (idx == n - 1 || keys_in[idx + 1] != k) atomicMax(&fin.ranges[k].y, (uint32_t)(idx + 1));
             }
         }
+#ifdef GSR_SORT_TRACE
+        __syncthreads();
+        if (threadIdx.x == 0 && t < 1024) {
+            unsigned long long* w = g_gsr_strace[(shift >> 3) & 3][t];
+            w[0] = st0; w[1] = st1; w[2] = 0; w[3] = 0; w[4] = __builtin_amdgcn_s_memrealtime();
+            w[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 15u;
+        }
+#endif
         return;
     }
 #pragma unroll
@@ -435,6 +478,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
         if (valid && rank == 0) wcnt[wid][digit] = old + (uint32_t)__popcll(peers);
     }
     __syncthreads();
+    ST_T(st2)
     // digit-major block offsets: dbase[d] = elements of digits < d; wave offsets inside d
     uint32_t tot = 0;
     if ((uint32_t)tid < ndig)
@@ -471,6 +515,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
         }
     }
     __syncthreads();
+    ST_T(st3)
 #pragma unroll
     for (int r = 0; r < ITEMS; ++r) {
         const size_t idx = wbase + (size_t)r * 64 + lane;
@@ -498,6 +543,217 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
             if (p == nvalid - 1 || s_key[p + 1] != k) atomicMax(&fin.ranges[k].y, (uint32_t)(g + 1));
         }
     }
+#ifdef GSR_SORT_TRACE
+    if (LB) {
+        __syncthreads();
+        if (threadIdx.x == 0 && t < 1024) {
+            unsigned long long* w = g_gsr_strace[(shift >> 3) & 3][t];
+            w[0] = st0; w[1] = st1; w[2] = st2; w[3] = st3; w[4] = __builtin_amdgcn_s_memrealtime();
+            w[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 15u;
+        }
+    }
+#endif
+}
+
+// ------------------------------------------- grouped look-back passes ----
+// The depth sort's passes for grids of at most GRP_MAX_TILES tiles (1M keys at 4096 keys per
+// tile), measured per tile phase (tools/sort_trace.py, profiles/round3_sort_trace.txt): of a
+// 17.8-us pass, 2.1 us went to the atomic that hands out tile indices, 6.8 us to the decoupled
+// look-back (the inclusive prefix advanced 8 tiles per cross-XCD round trip: the last tiles
+// finished their look-back 9 us after the first), and identity passes (a constant top byte)
+// still cost a 7-us copy plus a launch gap.  Here:
+//   * tile index = blockIdx.x.  Tile t waits only on tiles < t; the dispatcher starts a
+//     kernel's workgroups in index order on each XCD, so the lowest unfinished tile has always
+//     started and its predecessors have finished: the waits terminate (and with <= 256 tiles
+//     of 1024 threads, every tile is resident at once anyway);
+//   * two-level look-back: a tile publishes its digit counts, sums those of the earlier tiles
+//     of its group of GRP_SIZE (independent loads, no chain), and the group's last tile
+//     publishes the group total; a tile adds the totals of the earlier groups.  About three
+//     round trips instead of one per 8 tiles;
+//   * the pass plan comes from the digit spans of every pass (k_radix_hist): passes that are
+//     the identity on the keys that matter return at once, and the real passes ping-pong so
+//     that the last real one writes the output arrays (buffers chosen on the device: no copy).
+// Results are identical to the other modes (same stable order on the keys that matter).
+constexpr int GRP_SIZE = 16, GRP_MAX_TILES = GRP_SIZE * GRP_SIZE;
+struct GrpBufs {
+    const uint32_t* kin;
+    const uint32_t* v2in;
+    uint32_t *ktmp, *vtmp, *v2tmp;
+    uint32_t *kout, *vout, *v2out;
+};
+template <int ITEMS, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES) k_radix_scatter_grp(GrpBufs B, size_t n, int pass, int passes,
+                                                                  int per_pass, int key_bits,
+                                                                  const uint32_t* __restrict__ hist,
+                                                                  uint64_t* status, const uint32_t* span,
+                                                                  int no_keys) {
+    constexpr int NT = 64 * WAVES, TILE = NT * ITEMS;
+    ST_T(st0)
+    __shared__ uint32_t s_key[TILE], s_val[TILE], s_val2[TILE];
+    __shared__ uint32_t wcnt[WAVES][RADIX];
+    __shared__ uint32_t dbase[RADIX], gbase[RADIX];
+    __shared__ uint32_t wsum[WAVES];
+    const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+    const int t = (int)blockIdx.x, ntiles = (int)gridDim.x;
+    // the pass plan: real passes (span: max(256 - d) / max(d + 1) over the keys that matter)
+    int nreal = 0, j = -1;
+    for (int p = 0; p < passes; ++p) {
+        const uint32_t lo = span[2 * p], hi = span[2 * p + 1];
+        const bool real = !(lo == 0u || 256u - lo == hi - 1u);
+        if (real) {
+            if (p == pass) j = nreal;
+            ++nreal;
+        }
+    }
+    if (nreal == 0 && pass == 0) {  // every pass is the identity: pass 0 runs (a stable copy)
+        nreal = 1;
+        j = 0;
+    }
+    ST_T(st1)
+    if (j < 0) return;  // uniform: identity pass
+    const bool to_out = ((nreal - 1 - j) & 1) == 0, from_out = j > 0 && ((nreal - j) & 1) == 0;
+    const uint32_t* keys_in = j == 0 ? B.kin : (from_out ? B.kout : B.ktmp);
+    const uint32_t* vals_in = j == 0 ? nullptr : (from_out ? B.vout : B.vtmp);
+    const uint32_t* vals2_in = j == 0 ? B.v2in : (from_out ? B.v2out : B.v2tmp);
+    const bool last = j == nreal - 1;
+    uint32_t* keys_out = to_out ? ((last && no_keys) ? nullptr : B.kout) : B.ktmp;
+    uint32_t* vals_out = to_out ? B.vout : B.vtmp;
+    uint32_t* vals2_out = B.v2in ? (to_out ? B.v2out : B.v2tmp) : nullptr;
+    const int shift = pass * per_pass;
+    const int bits = min(per_pass, key_bits - shift);
+    const uint32_t ndig = 1u << bits, mask = ndig - 1u;
+#pragma unroll
+    for (int i = 0; i < RADIX / 64; ++i) wcnt[wid][lane + 64 * i] = 0;
+    const size_t bbase = (size_t)t * TILE;
+    const size_t wbase = bbase + (size_t)wid * (64 * ITEMS);
+    const uint64_t lt = lanemask_lt();
+    uint32_t key[ITEMS], val[ITEMS], val2[ITEMS], rk[ITEMS];
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const size_t idx = wbase + (size_t)r * 64 + lane;
+        const bool valid = idx < n;
+        key[r] = valid ? keys_in[idx] : 0u;
+        val[r] = valid ? (vals_in ? vals_in[idx] : (uint32_t)idx) : 0u;
+        val2[r] = (valid && vals2_in) ? vals2_in[idx] : 0u;
+    }
+    // the pass's global digit counts (used after the ranking), issued after the keys: the
+    // in-order load counter would otherwise make the ranking wait for this load as well
+    const uint32_t hcount = (uint32_t)tid < ndig ? hist[pass * RADIX + tid] : 0u;
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const size_t idx = wbase + (size_t)r * 64 + lane;
+        const bool valid = idx < n;
+        const uint32_t digit = (key[r] >> shift) & mask;
+        uint64_t peers = __ballot(valid);
+        for (int b = 0; b < bits; ++b) {
+            const bool set = (digit >> b) & 1u;
+            const uint64_t m = __ballot(set);
+            peers &= set ? m : ~m;
+        }
+        const uint32_t rank = __popcll(peers & lt);
+        const uint32_t old = valid ? wcnt[wid][digit] : 0u;
+        rk[r] = old + rank;
+        if (valid && rank == 0) wcnt[wid][digit] = old + (uint32_t)__popcll(peers);
+    }
+    __syncthreads();
+    ST_T(st2)
+    uint32_t tot = 0;
+    if ((uint32_t)tid < ndig)
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) tot += wcnt[w][tid];
+    if ((uint32_t)tid < ndig) {  // publish this tile's digit counts first: later tiles wait on them
+        uint64_t* agg = status + (size_t)t * RADIX + tid;
+        lb_store(agg, LB_AGG | tot);
+    }
+    uint32_t total;
+    const uint32_t db = block_exclusive_scan_w<WAVES>(tot, wsum, &total);
+    const uint32_t gstart = block_exclusive_scan_w<WAVES>(hcount, wsum, &total);
+    if ((uint32_t)tid < ndig) {
+        dbase[tid] = db;
+        uint32_t o = db;
+#pragma unroll
+        for (int w = 0; w < WAVES; ++w) {
+            const uint32_t cw = wcnt[w][tid];
+            wcnt[w][tid] = o;
+            o += cw;
+        }
+        const int g = t / GRP_SIZE, t0 = g * GRP_SIZE;
+        uint64_t* const aggs = status + tid;                                  // [tile][RADIX]
+        uint64_t* const grps = status + (size_t)ntiles * RADIX + tid;         // [group][RADIX]
+        // earlier tiles of the group: all loads issued together, re-issued until published
+        uint32_t in_grp = 0;
+        for (int i = t0; i < t;) {
+            uint64_t w[GRP_SIZE];
+#pragma unroll
+            for (int k = 0; k < GRP_SIZE; ++k) w[k] = i + k < t ? lb_load(aggs + (size_t)(i + k) * RADIX) : LB_AGG;
+            bool stall = false;
+#pragma unroll
+            for (int k = 0; k < GRP_SIZE; ++k) {
+                if (stall || i + k >= t) continue;
+                if ((w[k] >> 32) == 0) {
+                    stall = true;
+                    continue;
+                }
+                in_grp += (uint32_t)w[k];
+            }
+            if (!stall) break;
+            // restart the group sum: some word was not published yet
+            in_grp = 0;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        if (t == t0 + GRP_SIZE - 1 && t + 1 < ntiles)  // the group's total, for the later groups
+            lb_store(grps + (size_t)g * RADIX, LB_AGG | (in_grp + tot));
+        uint32_t before = 0;
+        for (int i = 0; i < g;) {
+            uint64_t w[GRP_SIZE];
+#pragma unroll
+            for (int k = 0; k < GRP_SIZE; ++k) w[k] = i + k < g ? lb_load(grps + (size_t)(i + k) * RADIX) : LB_AGG;
+            bool stall = false;
+#pragma unroll
+            for (int k = 0; k < GRP_SIZE; ++k) {
+                if (stall || i + k >= g) continue;
+                if ((w[k] >> 32) == 0) {
+                    stall = true;
+                    continue;
+                }
+                before += (uint32_t)w[k];
+            }
+            if (!stall) break;
+            before = 0;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        gbase[tid] = gstart + before + in_grp;
+    }
+    __syncthreads();
+    ST_T(st3)
+#pragma unroll
+    for (int r = 0; r < ITEMS; ++r) {
+        const size_t idx = wbase + (size_t)r * 64 + lane;
+        if (idx < n) {
+            const uint32_t pos = wcnt[wid][(key[r] >> shift) & mask] + rk[r];
+            s_key[pos] = key[r];
+            s_val[pos] = val[r];
+            s_val2[pos] = val2[r];
+        }
+    }
+    __syncthreads();
+    const int nvalid = bbase < n ? (int)min((size_t)TILE, n - bbase) : 0;
+    for (int p = tid; p < nvalid; p += NT) {
+        const uint32_t k = s_key[p];
+        const uint32_t d = (k >> shift) & mask;
+        const size_t g = (size_t)gbase[d] + (uint32_t)p - dbase[d];
+        if (keys_out) keys_out[g] = k;
+        vals_out[g] = s_val[p];
+        if (vals2_out) vals2_out[g] = s_val2[p];
+    }
+#ifdef GSR_SORT_TRACE
+    __syncthreads();
+    if (threadIdx.x == 0 && t < 1024) {
+        unsigned long long* w = g_gsr_strace[pass & 3][t];
+        w[0] = st0; w[1] = st1; w[2] = st2; w[3] = st3; w[4] = __builtin_amdgcn_s_memrealtime();
+        w[5] = __builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 15u;
+    }
+#endif
 }
 
 // ----------------------------------------------------------- duplicate ----
@@ -735,6 +991,12 @@ int sort_lb_items() { return GSR_LB_ITEMS * GSR_LB_WAVES / 4; }  // in units of 
 static size_t g_sort_lb_max = GSR_SORT_LB_MAX;  // gsr_set_option("sort_lookback_max", n)
 void set_sort_lookback_max(size_t n) { g_sort_lb_max = n; }
 bool sort_uses_lookback(size_t n) { return n <= g_sort_lb_max; }
+#ifndef GSR_SORT_GROUPED
+#define GSR_SORT_GROUPED 1
+#endif
+static bool g_sort_grouped = GSR_SORT_GROUPED;  // gsr_set_option("sort_grouped", 0 / 1)
+void set_sort_grouped(bool on) { g_sort_grouped = on; }
+size_t sort_grp_status_words(size_t nt) { return (nt + cdiv(nt, GRP_SIZE)) * RADIX; }
 
 // A tile is 64 * WAVES * ITEMS elements; sort_tiles(n, WAVES * ITEMS / 4) counts them.
 template <int ITEMS, int WAVES, bool LB>
@@ -761,11 +1023,24 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     const int per_pass = (key_bits + passes - 1) / passes;  // balanced: 13 bits -> 7 + 6
     const SortWs W = sort_ws(n, ws);
     const bool lb = sort_uses_lookback(n);
+    const bool grp = lb && g_sort_grouped && !n_dev && sort_tiles(n, sort_lb_items()) <= (size_t)GRP_MAX_TILES &&
+                     (!final_out || (!final_out->ranges && final_out->zero16 == 0));
     if (lb) {
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);
         hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)cdiv(n, (size_t)HIST_THREADS * HIST_ITEMS)), dim3(HIST_THREADS), 0, st, keys_in,
                            n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel, n_dev);
+    }
+    if (grp && !vals_in) {
+        // grouped look-back passes with the pass plan on the device (k_radix_scatter_grp)
+        const size_t nt = sort_tiles(n, sort_lb_items());
+        const GrpBufs B{keys_in, vals2_in, keys_tmp, vals_tmp, vals2_tmp, keys_out, vals_out, vals2_out};
+        const int no_keys = final_out && final_out->no_keys ? 1 : 0;
+        for (int p = 0; p < passes; ++p)
+            hipLaunchKernelGGL((k_radix_scatter_grp<GSR_LB_ITEMS, GSR_LB_WAVES>), dim3((unsigned)nt),
+                               dim3(64 * GSR_LB_WAVES), 0, st, B, n, p, passes, per_pass, key_bits, W.hist,
+                               W.status + (size_t)p * sort_grp_status_words(nt), W.counter + SPAN_WORD, no_keys);
+        return;
     }
     const uint32_t* kin = keys_in;
     const uint32_t* vin = vals_in;

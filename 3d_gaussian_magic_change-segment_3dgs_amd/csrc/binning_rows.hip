@@ -32,6 +32,31 @@
 // the metric scene), against ~52 for duplicate + two radix passes over (key, slot, id).
 #include "gsr_internal.h"
 
+#ifdef GSR_SORT_TRACE
+// Timeline build (tools/sort_trace.py): per block of k_rows_scatter [0], k_tiles_count [1] and
+// k_tiles_scatter [2]: s_memrealtime at entry, after the row map, at the end, chunks | XCC << 16.
+__device__ unsigned long long g_gsr_btrace[3][4096][4];
+extern "C" __attribute__((visibility("default"))) int gsr_bin_trace_read(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gsr_btrace), sizeof(g_gsr_btrace)) != hipSuccess) return -1;
+    if (reset) {
+        void* d = nullptr;
+        if (hipGetSymbolAddress(&d, HIP_SYMBOL(g_gsr_btrace)) != hipSuccess) return -1;
+        if (hipMemset(d, 0, sizeof(g_gsr_btrace)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+#define BT_T(var) const unsigned long long var = __builtin_amdgcn_s_memrealtime();
+#define BT_END(k, t0, t1, nch)                                                                          \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) {                                                       \
+        unsigned long long* w_ = g_gsr_btrace[k][blockIdx.x];                                          \
+        w_[0] = t0; w_[1] = t1; w_[2] = __builtin_amdgcn_s_memrealtime();                              \
+        w_[3] = (unsigned long long)(nch) | ((unsigned long long)(__builtin_amdgcn_s_getreg((20) | (0 << 6) | (3 << 11)) & 15u) << 16); \
+    }
+#else
+#define BT_T(var)
+#define BT_END(k, t0, t1, nch)
+#endif
+
 namespace gsr {
 
 namespace {
@@ -154,6 +179,7 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_scatter(int P, int gy, int nch1
     __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
     __shared__ uint32_t s_gid[RB_STAGE1], s_u[RB_STAGE1], s_x[RB_STAGE1];
     __shared__ uint32_t tot;
+    BT_T(bt0)
     const int tid = threadIdx.x;
     const int r = blockIdx.x * RB_CH1 + tid;
     int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
@@ -207,6 +233,7 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_scatter(int P, int gy, int nch1
             e_x[gp] = xr & 0xFFFFu;
         }
     }
+    BT_END(0, bt0, bt0, 1)
 }
 
 // ---------------------------------------------------------------- level 2 --
@@ -257,12 +284,16 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_count(int gx, int gy, int nch1,
     __shared__ int d[RB_MAXB + 1];
     __shared__ uint32_t e[RB_MAXB + 1];
     __shared__ uint32_t tot;
+    BT_T(bt0)
     zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH + threadIdx.x, (size_t)gridDim.x * RB_CH);  // scan-2 words
     for (int t = blockIdx.x * RB_CH + threadIdx.x; t < gx * gy; t += gridDim.x * RB_CH) ranges[t] = make_uint2(0u, 0u);
     if (blockIdx.x == 0 && threadIdx.x < TILE_BUCKET_WORDS) bucket_words[threadIdx.x] = 0u;
     build_row_map(m, gy, nch1, table1, base1, cap);
+    BT_T(bt1)
     if (blockIdx.x == 0 && threadIdx.x == 0) *len2 = (uint32_t)gx * m.nch2;
+    uint32_t nch_ = 0;
     for (uint32_t c = blockIdx.x; c < m.nch2; c += gridDim.x) {
+        ++nch_;
         const int y = chunk_row(m, gy, c);
         const uint32_t s = c - m.c0[y], e0 = m.rs[y] + s * RB_CH, n = min((uint32_t)RB_CH, m.rs[y + 1] - e0);
         for (int i = threadIdx.x; i <= gx; i += RB_CH) d[i] = 0;
@@ -277,6 +308,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_count(int gx, int gy, int nch1,
         for (int x = threadIdx.x; x < gx; x += RB_CH) table2[tile_slot(m, gx, y, x, s)] = e[x + 1];
         __syncthreads();
     }
+    BT_END(1, bt0, bt1, nch_)
 }
 
 // point_list / slot_vals; the ranges of every non-empty row (from the chunk s = 0 of the
@@ -305,10 +337,13 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
     __shared__ uint8_t s_x[RB_STAGE];
     __shared__ uint32_t tot;
     __shared__ uint32_t s_bc[33];  // this row's tiles per schedule bucket (k_tile_order_counted)
+    BT_T(bt0)
     const int tid = threadIdx.x;
     for (size_t i = (size_t)blockIdx.x * RB_CH + tid; i < nzero16; i += (size_t)gridDim.x * RB_CH)
         zero[i] = make_uint4(0u, 0u, 0u, 0u);
     build_row_map(m, gy, nch1, table1, base1, cap);
+    BT_T(bt1)
+    uint32_t nch_ = 0;
     const uint32_t len2 = (uint32_t)gx * m.nch2, itot = min(*n_total, cap);
     const uint32_t bit = 1u << (tid & 31), wd = (uint32_t)tid >> 5, below = bit - 1u;
     // chunk c -> its row, sub-chunk, entries, this thread's entry and bucket base (prefetch)
@@ -398,7 +433,9 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
         __syncthreads();
         c = cn;
         cur = nxt;
+        ++nch_;
     }
+    BT_END(2, bt0, bt1, nch_)
 }
 
 }  // namespace

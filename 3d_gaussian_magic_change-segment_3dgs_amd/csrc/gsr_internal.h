@@ -94,9 +94,14 @@ inline size_t sort_ws_bytes(size_t n, int passes) {
     const size_t tb = align_up(nt * RADIX * 4) + scan_ws_bytes(nt * RADIX);
     return ALIGN + align_up((size_t)MAX_SORT_PASSES * RADIX * 4) + (lb > tb ? lb : tb);
 }
-// Bytes of the workspace a look-back sort of n keys in `passes` passes needs zeroed.
+// Status words of one grouped look-back pass over nt tiles (binning.hip: per tile, then per
+// group of tiles, RADIX words each).
+size_t sort_grp_status_words(size_t nt);
+// Bytes of the workspace a look-back sort of n keys in `passes` passes needs zeroed (either
+// look-back mode: the grouped one's status words are the larger).
 inline size_t sort_lb_zero_bytes(size_t n, int passes, int items) {
-    return ALIGN + align_up((size_t)MAX_SORT_PASSES * RADIX * 4) + (size_t)passes * sort_tiles(n, items) * RADIX * 8;
+    return ALIGN + align_up((size_t)MAX_SORT_PASSES * RADIX * 4) +
+           (size_t)passes * sort_grp_status_words(sort_tiles(n, items)) * 8;
 }
 inline SortWs sort_ws(size_t n, void* p) {
     char* c = static_cast<char*>(p);
@@ -285,6 +290,7 @@ int depth_sort_passes();
 int sort_lb_items();
 bool sort_uses_lookback(size_t n);
 void set_sort_lookback_max(size_t n);
+void set_sort_grouped(bool on);  // grouped look-back passes for sorts of <= 256 tiles (default on)
 // Both tile-order launchers also write order[T + SCHED_FWD_SPLIT]: the number of tiles in
 // length buckets >= the forward's split bucket (set_split_buckets; 0 = no split), and zero
 // the backward queue's counters (TileSched).  bwd_depth: the backward splits tiles whose

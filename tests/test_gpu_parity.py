@@ -244,6 +244,38 @@ def test_table_mode_sorts(gpu_available, oracle_mod):
         _C.set_option("sort_lookback_max", 4 << 20)
 
 
+@pytest.mark.parametrize("case", ["narrow", "wide", "flat"])
+def test_depth_sort_grouped_matches_lookback(gpu_available, oracle_mod, case):
+    """The depth sort's grouped look-back passes (binning.hip k_radix_scatter_grp: tile index =
+    block index, two-level look-back, identity passes skipped with the buffers routed on the
+    device) against the classic decoupled look-back passes: the whole depth order (culled
+    Gaussians included), point_list, ranges, n_contrib and the images bit for bit.  narrow:
+    depths 2.5-5.5 (the top key byte is constant: pass 3 is skipped); wide: depths 0.2-35
+    (every byte varies: four real passes); flat: every Gaussian at one depth (every pass is
+    the identity: pass 0 runs as a stable copy), also against the oracle (ties by index)."""
+    from diff_gaussian_rasterization import _C
+    if case == "wide":
+        scene = synthetic_scene(60000, sh_degree=1, seed=52, extent=30.0, log_scale=math.log(0.2))
+    else:
+        scene = synthetic_scene(60000, sh_degree=1, seed=51)
+        if case == "flat":
+            scene.means3D[:, 2] = 0.0
+    cam = orbit_camera(0, 640, 360, 400.0)
+    out = {}
+    try:
+        for mode in (1, 0):
+            _C.set_option("sort_grouped", mode)
+            out[mode] = Hn.run_gsr(scene, cam)
+    finally:
+        _C.set_option("sort_grouped", 1)
+    a, b = out[1], out[0]
+    assert a["num_rendered"] == b["num_rendered"] > 0
+    for k in ("order", "point_list", "ranges", "n_contrib", "color", "depth", "alpha", "segment"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    if case == "flat":
+        compare(oracle_mod, scene, cam)
+
+
 def test_grid_wider_than_packed_rect(gpu_available, oracle_mod):
     """More than 255 tiles across (4160 px): the tile rect does not fit the packed 8-bit
     form the depth sort carries, so the scan gathers tiles_touched by depth order and the
