@@ -260,16 +260,30 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restric
 // ---------------------------------------------------------- radix sort ----
 // Digit histograms of every pass at once (one read of the keys): LDS counters per
 // block, then one global atomic per (pass, digit, block).  hist[p * RADIX + d].
-// Also the digit range of every pass over the keys that matter (all keys, or all but
-// the 0xFFFFFFFF sentinel when skip_sentinel: culled Gaussians of the depth sort, whose
-// position is irrelevant): span[2p] = max(256 - d), span[2p + 1] = max(d + 1) (zero-
-// initialised words).  A pass whose keys that matter all share one digit is the
-// identity on them and is skipped (k_radix_scatter copies the tile through).
+// Also which key bits vary over the keys that matter (all keys, or all but the 0xFFFFFFFF
+// sentinel when skip_sentinel: culled Gaussians of the depth sort, whose position is
+// irrelevant): span[0] = OR of the keys, span[1] = OR of their complements (zero-initialised
+// words), so bit b varies iff it is set in span[0] & span[1].  A pass whose digit bits are all
+// constant over the keys that matter is the identity on them and is skipped (identity_pass).
+// The ORs are wave-reduced with DPP row rotations and four v_readlane (round 2 took min / max
+// digit spans per pass with 48 dependent lane shuffles per wave: 6.8 us of LDS phase per block).
 // Keys per thread of k_radix_hist: fewer, fuller blocks mean fewer global atomics at the
 // end (one per nonzero (pass, digit) per block).
 // 16 waves x 4 keys per thread per block (a 4-wave block with 16 keys per thread left
 // under one wave per SIMD at 1M keys: latency-bound, 16 us).
 constexpr int HIST_THREADS = 1024, HIST_ITEMS = 4;
+__device__ __forceinline__ uint32_t wave_or(uint32_t x) {
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x121, 0xF, 0xF, false);  // row_ror:1
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x122, 0xF, 0xF, false);  // row_ror:2
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xF, 0xF, false);  // row_ror:4
+    x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);  // row_ror:8
+    return (uint32_t)__builtin_amdgcn_readlane((int)x, 0) | (uint32_t)__builtin_amdgcn_readlane((int)x, 16) |
+           (uint32_t)__builtin_amdgcn_readlane((int)x, 32) | (uint32_t)__builtin_amdgcn_readlane((int)x, 48);
+}
+// A pass over digit bits [shift, shift + bits) is the identity on the keys that matter.
+__device__ __forceinline__ bool identity_pass(const uint32_t* span, int shift, int bits) {
+    return (((span[0] & span[1]) >> shift) & ((1u << bits) - 1u)) == 0u;
+}
 __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __restrict__ keys, size_t n,
                                                              int passes, int per_pass, int key_bits,
                                                              uint32_t* __restrict__ hist, uint32_t* span,
@@ -277,13 +291,13 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
     ST_T(st0)
     if (n_dev) n = min(n, (size_t)*n_dev);
     __shared__ uint32_t cnt[4][RADIX];
-    __shared__ uint32_t s_span[8];
+    __shared__ uint32_t s_span[2];
     if (threadIdx.x < RADIX)
 #pragma unroll
         for (int p = 0; p < 4; ++p) cnt[p][threadIdx.x] = 0;
-    if (threadIdx.x < 8) s_span[threadIdx.x] = 0;
+    if (threadIdx.x < 2) s_span[threadIdx.x] = 0;
     __syncthreads();
-    uint32_t lo[4] = {0, 0, 0, 0}, hi[4] = {0, 0, 0, 0};  // max(256 - d), max(d + 1)
+    uint32_t ork = 0, ornk = 0;
     // all loads issued before any use (a strided loop with one dependent load per
     // iteration is latency-bound)
     const size_t base = (size_t)blockIdx.x * HIST_THREADS * HIST_ITEMS + threadIdx.x;
@@ -304,16 +318,16 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
         const uint32_t k = kk[i];
         const uint64_t vmask = __ballot(valid);
         const bool matters = valid && !(skip_sentinel && k == 0xFFFFFFFFu);
+        if (matters) {
+            ork |= k;
+            ornk |= ~k;
+        }
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             if (p >= passes) break;
             const int shift = p * per_pass;
             const int bits = min(per_pass, key_bits - shift);
             const uint32_t d = (k >> shift) & ((1u << bits) - 1u);
-            if (matters) {
-                lo[p] = max(lo[p], 256u - d);
-                hi[p] = max(hi[p], d + 1u);
-            }
             // wave-aggregated: a digit shared by the whole wave (the high digits of keys
             // with a narrow range) is one LDS atomic, not 64 serialised on one address
             const uint32_t d0 = __builtin_amdgcn_readfirstlane(d);
@@ -324,24 +338,18 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
             }
         }
     }
-#pragma unroll
-    for (int p = 0; p < 4; ++p) {
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-            lo[p] = max(lo[p], (uint32_t)__shfl_xor((int)lo[p], o, 64));
-            hi[p] = max(hi[p], (uint32_t)__shfl_xor((int)hi[p], o, 64));
-        }
-        if ((threadIdx.x & 63) == 0 && p < passes) {
-            atomicMax(&s_span[2 * p], lo[p]);
-            atomicMax(&s_span[2 * p + 1], hi[p]);
-        }
+    ork = wave_or(ork);
+    ornk = wave_or(ornk);
+    if ((threadIdx.x & 63) == 0) {
+        if (ork) atomicOr(&s_span[0], ork);
+        if (ornk) atomicOr(&s_span[1], ornk);
     }
     __syncthreads();
     ST_T(st2)
     if (threadIdx.x < RADIX)
         for (int p = 0; p < passes; ++p)
             if (cnt[p][threadIdx.x]) atomicAdd(&hist[p * RADIX + threadIdx.x], cnt[p][threadIdx.x]);
-    if (threadIdx.x < 2 * passes && s_span[threadIdx.x]) atomicMax(&span[threadIdx.x], s_span[threadIdx.x]);
+    if (threadIdx.x < 2 && s_span[threadIdx.x]) atomicOr(&span[threadIdx.x], s_span[threadIdx.x]);
 #ifdef GSR_SORT_TRACE
     __syncthreads();
     if (threadIdx.x == 0 && blockIdx.x < 1024) {
@@ -418,11 +426,11 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
     __shared__ uint32_t wsum[WAVES];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const uint32_t ndig = 1u << bits, mask = ndig - 1u;
-    // span = this pass's digit range over the keys that matter (k_radix_hist)
-    const uint32_t sp_lo = LB && span ? span[0] : 0u, sp_hi = LB && span ? span[1] : 1u;
+    // span: the key bits that vary over the keys that matter (k_radix_hist)
+    const bool ident = LB && span && identity_pass(span, shift, bits);
     const int t = LB ? lb_tile_index(counter) : (int)blockIdx.x;
     ST_T(st1)
-    if (LB && span && (sp_lo == 0u || 256u - sp_lo == sp_hi - 1u)) {
+    if (ident) {
         // Every key that matters has the same digit in this pass: a stable pass is the
         // identity on them, so the tile is copied through and the look-back chain is
         // skipped.  Uniform over the grid.
@@ -595,11 +603,10 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter_grp(GrpBufs B, siz
     __shared__ uint32_t wsum[WAVES];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
     const int t = (int)blockIdx.x, ntiles = (int)gridDim.x;
-    // the pass plan: real passes (span: max(256 - d) / max(d + 1) over the keys that matter)
+    // the pass plan: real passes (span: the key bits that vary over the keys that matter)
     int nreal = 0, j = -1;
     for (int p = 0; p < passes; ++p) {
-        const uint32_t lo = span[2 * p], hi = span[2 * p + 1];
-        const bool real = !(lo == 0u || 256u - lo == hi - 1u);
+        const bool real = !identity_pass(span, p * per_pass, min(per_pass, key_bits - p * per_pass));
         if (real) {
             if (p == pass) j = nreal;
             ++nreal;
@@ -1061,7 +1068,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
             launch_scatter<GSR_LB_ITEMS, GSR_LB_WAVES, true>(n, kin, vin, kout, vout, shift, bits,
                                                              W.hist + p * RADIX, W.status + (size_t)p * nt * RADIX,
                                                              W.counter + p, v2in, v2out, fin,
-                                                             W.counter + SPAN_WORD + 2 * p, n_dev, st);
+                                                             W.counter + SPAN_WORD, n_dev, st);
         } else {
             const size_t nt = sort_tiles(n, GSR_TB_ITEMS * GSR_TB_WAVES / 4);
             const size_t len = ((size_t)1 << bits) * nt;

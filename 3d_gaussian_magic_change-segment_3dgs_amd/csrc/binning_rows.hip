@@ -64,15 +64,35 @@ namespace {
 constexpr int RB_CH1 = 1024;          // level 1: depth-ordered Gaussians per chunk = threads per block
 constexpr int RB_S1 = RB_CH1 / 32 + 1; // its LDS words per bucket row (bitmask words + pad)
 constexpr int RB_STAGE1 = 4 * RB_CH1;  // its row entries assembled in LDS (more: direct writes)
-constexpr int RB_CH = 512;            // level 2: row entries per chunk = threads per block
+#ifndef GSR_RB_CH
+#define GSR_RB_CH 512
+#endif
+#ifndef GSR_RB_GRID2
+#define GSR_RB_GRID2 2048
+#endif
+constexpr int RB_CH = GSR_RB_CH;      // level 2: row entries per chunk = threads per block
 constexpr int RB_W = RB_CH / 32;      // bitmask words per bucket
 // LDS words per bucket row of bits / pre: one pad word so that the words of different
 // buckets fall in different banks (with a stride of 16 words, lanes touching buckets 4
 // apart hit one bank: 13M bank-conflict cycles per tile-scatter launch at the metric scene)
 constexpr int RB_S = RB_W + 1;
-constexpr int RB_STAGE = 2048;        // outputs a chunk assembles in LDS (more: direct writes)
+constexpr int RB_STAGE = 4 * RB_CH;    // outputs a chunk assembles in LDS (more: direct writes)
 constexpr int RB_MAXB = 256;          // buckets per chunk (<= 255 rows / columns)
-constexpr int RB_GRID2 = 2048;        // blocks of the level-2 kernels (grid-stride over chunks)
+constexpr int RB_GRID2 = GSR_RB_GRID2;  // blocks of the level-2 kernels (grid-stride over chunks)
+
+// Inclusive scans of x over groups of W = 16, 32 or 64 consecutive lanes with DPP (row_shr
+// inside a 16-lane row, then row_bcast15 / row_bcast31 across rows): no LDS round trip per step
+// (the ds_bpermute shuffles they replace were the latency chain of every level-2 chunk).
+template <int W>
+__device__ __forceinline__ uint32_t scan_incl(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    if (W >= 32) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);  // row_bcast:15
+    if (W >= 64) x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false);  // row_bcast:31
+    return x;
+}
 
 // Exclusive scan of n <= 256 LDS values v[0..n) by wave 0 (4 values per lane): out[k] =
 // sum of v[0..k); *tot = sum of all.  Every thread of the block must call it (barrier).
@@ -86,12 +106,7 @@ __device__ void lds_scan256(const uint32_t* v, int n, uint32_t* out, uint32_t* t
             a[i] = k < n ? v[k] : 0u;
             s += a[i];
         }
-        uint32_t x = s;
-#pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-            if (l >= o) x += y;
-        }
+        const uint32_t x = scan_incl<64>(s);
         uint32_t e = x - s;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -107,23 +122,26 @@ __device__ void lds_scan256(const uint32_t* v, int n, uint32_t* out, uint32_t* t
 // bits[b * RB_S + w]: bit i of word w = item 32 w + i of the chunk covers bucket b.
 // pre[b * RB_S + w] = items of bucket b in words < w; cnt[b] = items of bucket b.
 // CH: items per chunk (= threads per block), CH / 32 bitmask words per bucket row of
-// CH / 32 + 1 LDS words.
+// CH / 32 + 1 LDS words.  Every word is loaded before the first scan (one LDS latency).
 template <int CH>
 __device__ void bucket_prefix(const uint32_t* bits, int nb, uint32_t* pre, uint32_t* cnt) {
     constexpr int W = CH / 32, S = W + 1;
+    constexpr int PER_WAVE = 64 / W, STEP = PER_WAVE * (CH / 64), ITER = (RB_MAXB + STEP - 1) / STEP;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    constexpr int PER_WAVE = 64 / W;  // buckets per wave pass
-    for (int b0 = PER_WAVE * wave; b0 < nb; b0 += PER_WAVE * (CH / 64)) {
-        const int b = b0 + lane / W, w = lane % W;
-        const uint32_t c = b < nb ? (uint32_t)__popc(bits[b * S + w]) : 0u;
-        uint32_t x = c;
+    const int bl = PER_WAVE * wave + lane / W, w = lane % W;
+    uint32_t c[ITER];
 #pragma unroll
-        for (int o = 1; o < W; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, o, W);
-            if (w >= o) x += y;
-        }
+    for (int i = 0; i < ITER; ++i) {
+        const int b = bl + i * STEP;
+        c[i] = b < nb ? (uint32_t)__popc(bits[b * S + w]) : 0u;
+    }
+#pragma unroll
+    for (int i = 0; i < ITER; ++i) {
+        if (i * STEP >= nb) break;  // uniform
+        const int b = bl + i * STEP;
+        const uint32_t x = scan_incl<W>(c[i]);
         if (b < nb) {
-            pre[b * S + w] = x - c;
+            pre[b * S + w] = x - c[i];
             if (w == W - 1) cnt[b] = x;
         }
     }
@@ -259,14 +277,18 @@ __device__ void build_row_map(RowMap& m, int gy, int nch1, const uint32_t* table
     if (tid == 0) m.c0[gy] = m.nch2;
     __syncthreads();
 }
-// row of chunk c (< nch2): the last row y with c0[y] <= c
+// row of chunk c (< nch2, block-uniform): the last row y with c0[y] <= c = the number of rows
+// y < gy with c0[y] <= c, minus one (c0 is non-decreasing, c0[0] = 0), counted by four
+// ballots per wave over independent LDS reads (a binary search was 8 dependent LDS reads)
 __device__ __forceinline__ int chunk_row(const RowMap& m, int gy, uint32_t c) {
-    int lo = 0, hi = gy;
-    while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (m.c0[mid] <= c) lo = mid; else hi = mid - 1;
-    }
-    return lo;
+    const int lane = threadIdx.x & 63;
+    uint32_t v[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) v[i] = lane + 64 * i < gy ? m.c0[lane + 64 * i] : 0xFFFFFFFFu;
+    int k = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) k += __popcll(__ballot(v[i] <= c));
+    return k - 1;
 }
 __device__ __forceinline__ size_t tile_slot(const RowMap& m, int gx, int y, int x, uint32_t s) {
     return (size_t)gx * m.c0[y] + (size_t)x * m.nsub[y] + s;  // (row, column, sub-chunk) order
@@ -309,6 +331,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_count(int gx, int gy, int nch1,
         __syncthreads();
     }
     BT_END(1, bt0, bt1, nch_)
+    (void)nch_;
 }
 
 // point_list / slot_vals; the ranges of every non-empty row (from the chunk s = 0 of the
@@ -333,8 +356,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
     uint32_t* pre = dyn + gx * RB_S;
     __shared__ RowMap m;
     __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
-    __shared__ uint32_t s_gid[RB_STAGE], s_u[RB_STAGE];
-    __shared__ uint8_t s_x[RB_STAGE];
+    __shared__ uint32_t s_gid[RB_STAGE], s_u[RB_STAGE], s_gp[RB_STAGE];
     __shared__ uint32_t tot;
     __shared__ uint32_t s_bc[33];  // this row's tiles per schedule bucket (k_tile_order_counted)
     BT_T(bt0)
@@ -410,7 +432,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
                     const uint32_t lp = lst[x] + rank;
                     s_gid[lp] = cur.g;
                     s_u[lp] = uu;
-                    s_x[lp] = (uint8_t)x;
+                    s_gp[lp] = gb[x] + rank;
                 } else {
                     const uint32_t gp = gb[x] + rank;
                     if (gp < cap) {
@@ -422,8 +444,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
         if (staged) {
             __syncthreads();
             for (uint32_t i = tid; i < tot; i += RB_CH) {
-                const uint32_t x = s_x[i];
-                const uint32_t gp = gb[x] + (i - lst[x]);
+                const uint32_t gp = s_gp[i];
                 if (gp < cap) {
                     point_list[gp] = s_gid[i];
                     slot_vals[gp] = s_u[i];
@@ -436,6 +457,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
         ++nch_;
     }
     BT_END(2, bt0, bt1, nch_)
+    (void)nch_;
 }
 
 }  // namespace

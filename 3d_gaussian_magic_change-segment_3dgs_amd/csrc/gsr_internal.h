@@ -75,7 +75,7 @@ inline ScanWs scan_ws(size_t n, void* p) {
     return {p, scan_ws_bytes(n), reinterpret_cast<uint32_t*>(c), reinterpret_cast<uint64_t*>(c + ALIGN)};
 }
 // Sort workspace header: words [0, passes) are the look-back tile counters, words
-// [SPAN_WORD, SPAN_WORD + 2 passes) the per-pass digit spans (k_radix_hist).
+// [SPAN_WORD, SPAN_WORD + 2) the OR of the keys and of their complements (k_radix_hist).
 constexpr int SPAN_WORD = 16;
 struct SortWs {
     void* base;
