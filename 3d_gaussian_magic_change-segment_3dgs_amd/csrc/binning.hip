@@ -619,11 +619,16 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter_grp(GrpBufs B, siz
     ST_T(st1)
     if (j < 0) return;  // uniform: identity pass
     const bool to_out = ((nreal - 1 - j) & 1) == 0, from_out = j > 0 && ((nreal - j) & 1) == 0;
-    const uint32_t* keys_in = j == 0 ? B.kin : (from_out ? B.kout : B.ktmp);
+    const bool last = j == nreal - 1;
+    // Keys: when the output key array is the input one (the depth sort, whose sorted keys are
+    // not needed: no_keys), a pass must never write the array it or an earlier pass reads from
+    // while other tiles may still be loading it, so the keys alternate tmp, in, tmp, ... from
+    // pass 0 on; otherwise they follow the values (the last real pass writes the output).
+    const bool kalias = B.kout == B.kin;
+    const uint32_t* keys_in = j == 0 ? B.kin : (kalias ? ((j & 1) ? B.ktmp : B.kin) : (from_out ? B.kout : B.ktmp));
+    uint32_t* keys_out = (last && no_keys) ? nullptr : (kalias ? ((j & 1) ? B.kout : B.ktmp) : (to_out ? B.kout : B.ktmp));
     const uint32_t* vals_in = j == 0 ? nullptr : (from_out ? B.vout : B.vtmp);
     const uint32_t* vals2_in = j == 0 ? B.v2in : (from_out ? B.v2out : B.v2tmp);
-    const bool last = j == nreal - 1;
-    uint32_t* keys_out = to_out ? ((last && no_keys) ? nullptr : B.kout) : B.ktmp;
     uint32_t* vals_out = to_out ? B.vout : B.vtmp;
     uint32_t* vals2_out = B.v2in ? (to_out ? B.v2out : B.v2tmp) : nullptr;
     const int shift = pass * per_pass;
@@ -1030,8 +1035,11 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     const int per_pass = (key_bits + passes - 1) / passes;  // balanced: 13 bits -> 7 + 6
     const SortWs W = sort_ws(n, ws);
     const bool lb = sort_uses_lookback(n);
+    // (an output key array that is the input one is supported only when the sorted keys are not
+    // wanted: k_radix_scatter_grp then alternates the keys between the input and tmp arrays)
     const bool grp = lb && g_sort_grouped && !n_dev && sort_tiles(n, sort_lb_items()) <= (size_t)GRP_MAX_TILES &&
-                     (!final_out || (!final_out->ranges && final_out->zero16 == 0));
+                     (!final_out || (!final_out->ranges && final_out->zero16 == 0)) &&
+                     (keys_out != keys_in || (final_out && final_out->no_keys));
     if (lb) {
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);

@@ -162,7 +162,6 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_count(int P, int gy, int nch1, 
     __shared__ int d[RB_MAXB + 1];
     __shared__ uint32_t e[RB_MAXB + 1];
     __shared__ uint32_t tot;
-    zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH1 + threadIdx.x, (size_t)gridDim.x * RB_CH1);  // scan-1 words
     for (int i = threadIdx.x; i <= gy; i += RB_CH1) d[i] = 0;
     __syncthreads();
     const int r = blockIdx.x * RB_CH1 + threadIdx.x;
@@ -177,6 +176,8 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_count(int P, int gy, int nch1, 
     __syncthreads();
     lds_scan256(reinterpret_cast<const uint32_t*>(d), gy + 1, e, &tot);  // e[y + 1] = rows' counts
     for (int y = threadIdx.x; y < gy; y += RB_CH1) table1[(size_t)y * nch1 + blockIdx.x] = e[y + 1];
+    // the scan's status words, cleared after the rect load (one in-order vmcnt for loads and stores)
+    zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH1 + threadIdx.x, (size_t)gridDim.x * RB_CH1);
 }
 
 // Level-1 entries (E1, grouped by row): e_gid = Gaussian id, e_u = its first instance slot
@@ -307,29 +308,54 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_count(int gx, int gy, int nch1,
     __shared__ uint32_t e[RB_MAXB + 1];
     __shared__ uint32_t tot;
     BT_T(bt0)
-    zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH + threadIdx.x, (size_t)gridDim.x * RB_CH);  // scan-2 words
-    for (int t = blockIdx.x * RB_CH + threadIdx.x; t < gx * gy; t += gridDim.x * RB_CH) ranges[t] = make_uint2(0u, 0u);
-    if (blockIdx.x == 0 && threadIdx.x < TILE_BUCKET_WORDS) bucket_words[threadIdx.x] = 0u;
     build_row_map(m, gy, nch1, table1, base1, cap);
     BT_T(bt1)
     if (blockIdx.x == 0 && threadIdx.x == 0) *len2 = (uint32_t)gx * m.nch2;
     uint32_t nch_ = 0;
-    for (uint32_t c = blockIdx.x; c < m.nch2; c += gridDim.x) {
+    // chunk c -> row, sub-chunk and this thread's entry (the next chunk's entry is loaded while
+    // the current one is counted, and waited for before the current chunk's stores: gfx950's
+    // vmcnt is one in-order counter for loads and stores)
+    struct Chunk {
+        int y;
+        uint32_t s, xr;
+        bool valid;
+    };
+    auto fetch = [&](uint32_t c) {
+        Chunk k;
+        k.y = chunk_row(m, gy, c);
+        k.s = c - m.c0[k.y];
+        const uint32_t e0 = m.rs[k.y] + k.s * RB_CH, n = min((uint32_t)RB_CH, m.rs[k.y + 1] - e0);
+        k.valid = threadIdx.x < n;
+        k.xr = k.valid ? e_x[e0 + threadIdx.x] : 0u;
+        return k;
+    };
+    uint32_t c = blockIdx.x;
+    Chunk cur{};
+    if (c < m.nch2) cur = fetch(c);
+    while (c < m.nch2) {
         ++nch_;
-        const int y = chunk_row(m, gy, c);
-        const uint32_t s = c - m.c0[y], e0 = m.rs[y] + s * RB_CH, n = min((uint32_t)RB_CH, m.rs[y + 1] - e0);
         for (int i = threadIdx.x; i <= gx; i += RB_CH) d[i] = 0;
         __syncthreads();
-        if (threadIdx.x < n) {
-            const uint32_t xr = e_x[e0 + threadIdx.x];
-            atomicAdd(&d[xr & 255u], 1);
-            atomicAdd(&d[(xr >> 8) & 255u], -1);
+        if (cur.valid) {
+            atomicAdd(&d[cur.xr & 255u], 1);
+            atomicAdd(&d[(cur.xr >> 8) & 255u], -1);
         }
+        const uint32_t cn = c + gridDim.x;
+        Chunk nxt{};
+        if (cn < m.nch2) nxt = fetch(cn);
         __syncthreads();
         lds_scan256(reinterpret_cast<const uint32_t*>(d), gx + 1, e, &tot);  // e[x + 1] = column counts
-        for (int x = threadIdx.x; x < gx; x += RB_CH) table2[tile_slot(m, gx, y, x, s)] = e[x + 1];
-        __syncthreads();
+        asm volatile("" ::"v"(nxt.xr));
+        for (int x = threadIdx.x; x < gx; x += RB_CH) table2[tile_slot(m, gx, cur.y, x, cur.s)] = e[x + 1];
+        // no barrier: d was last read before lds_scan256's barrier, e is rewritten after two more
+        c = cn;
+        cur = nxt;
     }
+    // clears for the next kernels, issued after this kernel's loads (one in-order vmcnt: stores
+    // ahead of the row map's loads would delay them)
+    zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH + threadIdx.x, (size_t)gridDim.x * RB_CH);  // scan-2 words
+    for (int t = blockIdx.x * RB_CH + threadIdx.x; t < gx * gy; t += gridDim.x * RB_CH) ranges[t] = make_uint2(0u, 0u);
+    if (blockIdx.x == 0 && threadIdx.x < TILE_BUCKET_WORDS) bucket_words[threadIdx.x] = 0u;
     BT_END(1, bt0, bt1, nch_)
     (void)nch_;
 }
@@ -361,8 +387,6 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
     __shared__ uint32_t s_bc[33];  // this row's tiles per schedule bucket (k_tile_order_counted)
     BT_T(bt0)
     const int tid = threadIdx.x;
-    for (size_t i = (size_t)blockIdx.x * RB_CH + tid; i < nzero16; i += (size_t)gridDim.x * RB_CH)
-        zero[i] = make_uint4(0u, 0u, 0u, 0u);
     build_row_map(m, gy, nch1, table1, base1, cap);
     BT_T(bt1)
     uint32_t nch_ = 0;
@@ -417,7 +441,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
             if (bk) atomicAdd(&s_bc[bk], 1u);
         }
         const uint32_t cn = c + gridDim.x;
-        Chunk nxt;
+        Chunk nxt{};
         if (cn < m.nch2) nxt = fetch(cn);  // in flight while this chunk is ranked
         __syncthreads();
         if (cur.s == 0 && tid < 33 && s_bc[tid]) atomicAdd(&bucket_words[tid], s_bc[tid]);
@@ -441,6 +465,11 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
                     }
                 }
             }
+        // The next chunk's prefetched values are waited for here, before this chunk's output
+        // stores: gfx950 counts loads and stores in one in-order vmcnt, so a first use after
+        // a store loop of unknown length becomes vmcnt(0) -- a wait for every store's
+        // acknowledgement once per chunk.
+        asm volatile("" ::"v"(nxt.g), "v"(nxt.u), "v"(nxt.xr), "v"(nxt.gbv));
         if (staged) {
             __syncthreads();
             for (uint32_t i = tid; i < tot; i += RB_CH) {
@@ -450,12 +479,18 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
                     slot_vals[gp] = s_u[i];
                 }
             }
+        } else {
+            __syncthreads();  // gb and bits are rewritten at the top of the next chunk
         }
-        __syncthreads();
+        // (staged: bits and gb were last read before the barrier above; the staging arrays
+        // are next written after three more barriers)
         c = cn;
         cur = nxt;
         ++nch_;
     }
+    // the backward's written-slot flags, cleared after this kernel's loads (in-order vmcnt)
+    for (size_t i = (size_t)blockIdx.x * RB_CH + tid; i < nzero16; i += (size_t)gridDim.x * RB_CH)
+        zero[i] = make_uint4(0u, 0u, 0u, 0u);
     BT_END(2, bt0, bt1, nch_)
     (void)nch_;
 }

@@ -88,15 +88,17 @@ struct SortWs {
 };
 constexpr int MIN_SORT_ITEMS = 4;
 inline size_t sort_tiles(size_t n, int items) { return n ? cdiv(n, (size_t)SORT_THREADS * items) : 0; }
+size_t sort_grp_status_words(size_t nt);
 inline size_t sort_ws_bytes(size_t n, int passes) {
     const size_t nt = sort_tiles(n, MIN_SORT_ITEMS);
-    const size_t lb = (size_t)passes * nt * RADIX * 8;
+    // look-back status words of either look-back mode (the grouped one adds a word row per group
+    // of tiles; sort_lb_zero_bytes must never exceed this)
+    const size_t lb = (size_t)passes * sort_grp_status_words(nt) * 8;
     const size_t tb = align_up(nt * RADIX * 4) + scan_ws_bytes(nt * RADIX);
     return ALIGN + align_up((size_t)MAX_SORT_PASSES * RADIX * 4) + (lb > tb ? lb : tb);
 }
 // Status words of one grouped look-back pass over nt tiles (binning.hip: per tile, then per
 // group of tiles, RADIX words each).
-size_t sort_grp_status_words(size_t nt);
 // Bytes of the workspace a look-back sort of n keys in `passes` passes needs zeroed (either
 // look-back mode: the grouped one's status words are the larger).
 inline size_t sort_lb_zero_bytes(size_t n, int passes, int items) {

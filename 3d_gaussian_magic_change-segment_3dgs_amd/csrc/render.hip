@@ -538,6 +538,7 @@ __device__ __forceinline__ float fdiv(float num, float den) {
 struct BwdShared {
     float4 srec[2][64][4];  // per wave: the batch's records
     float part[2][64][12];  // split tiles: per-wave partial record of each batch instance
+    float4 stage[2][64][3]; // unsplit tiles: per-wave records of the batch, stored at the next batch
     uint64_t tmask[2];      // split tiles: instances each wave produced a partial for
     uint32_t top[2];        // split tiles: per-wave deepest contributor | use_bg << 31
 };
@@ -566,7 +567,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                                          const float* __restrict__ dL_ddepths,
                                          const float* __restrict__ dL_dalphas,
                                          float* __restrict__ contrib, uint8_t* __restrict__ written,
-                                         float4 (*srec)[4], BwdShared* sh) {
+                                         float4 (*srec)[4], BwdShared* sh, float4 (*stage)[3] = nullptr) {
 #pragma clang fp contract(off)
     WT_BEGIN
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -660,11 +661,32 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
     }
     // The background term of dL_dalpha (backward.cu:597) is only live when bg . dL_dpix
     // is non-zero somewhere in the tile: the loop is specialised on it.
+    // Unsplit tiles park a batch's records in LDS (stage[j] = record of batch instance j) and
+    // store them at the start of the next batch, ahead of its prefetch loads.  gfx950 counts
+    // vector loads and stores in one in-order vmcnt: with the records stored inside the batch,
+    // taking over the prefetched batch at its end waited for every record store's
+    // acknowledgement (an s_waitcnt vmcnt(0) per batch).
+    uint64_t prev_touched = 0;
+    uint32_t prev_uslot = 0;
+    auto flush = [&]() {
+        if constexpr (!SPLIT) {
+            if ((prev_touched >> lane) & 1ull) {
+                float4* d = reinterpret_cast<float4*>(contrib + (size_t)prev_uslot * 12);
+                const float4 a = stage[lane][0], b = stage[lane][1], c = stage[lane][2];
+                d[0] = a;
+                d[1] = b;
+                d[2] = c;
+                // byte u marks slot u as written
+                written[prev_uslot] = 1;
+            }
+        }
+    };
     auto replay = [&](auto use_bg_c) {
         constexpr bool UB = decltype(use_bg_c)::value;
         for (int top = top0; top > 0; top -= 64) {
             const int cnt = min(64, top);
             STAT(5, 1);
+            flush();
             const Batch nxt = fetch_batch(rec, g_next);
             const uint32_t u_nxt = u_next;
             g_next = plist[max(top - 129 - lane, 0)];
@@ -705,7 +727,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
             srec[lane][2] = rc;                                                   // r, g, b, seg1
             srec[lane][3] = make_float4(rb.z, __uint_as_float(uslot), 0.f, 0.f);  // depth, record slot
             wave_lds_sync();
-            uint64_t touched = 0;  // SPLIT: instances with a partial record from this wave
+            uint64_t touched = 0;  // instances with a (partial, SPLIT) record from this wave
             while (todo) {
                 const int j = (int)__builtin_ctzll(todo);
                 todo &= todo - 1;
@@ -825,14 +847,14 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                 const float r = wave_reduce12(acc, lane, vidx, valid);
                 if constexpr (SPLIT) {
                     if (valid) sh->part[wid][j][vidx] = r;
-                    touched |= 1ull << j;
                 } else {
-                    const uint32_t u = __float_as_uint(q3.y);
-                    if (valid) contrib[(size_t)u * 12 + vidx] = r;
-                    // Byte u marks slot u as written: one plain store of one byte by the whole
-                    // wave (a uniform address; no atomic, no lane election).
-                    written[u] = 1;
+                    if (valid) reinterpret_cast<float*>(stage[j])[vidx] = r;
                 }
+                touched |= 1ull << j;
+            }
+            if constexpr (!SPLIT) {
+                prev_touched = touched;
+                prev_uslot = uslot;
             }
             if constexpr (SPLIT) {
                 if (lane == 0) sh->tmask[wid] = touched;
@@ -862,6 +884,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
         replay(std::true_type{});
     else
         replay(std::false_type{});
+    flush();
     STAT_FLUSH(16)
     WT_END(1, wslot, tile, n, top0, NS)
 }
@@ -915,7 +938,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k
     } else {
         bwd_tile<4, false>(W, H, gx, tile, 0, (int)(2 * b + wid), ranges, point_list, slot_vals, rec, bg, alphas,
                            n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, sh.srec[wid],
-                           nullptr);
+                           nullptr, sh.stage[wid]);
     }
 }
 
@@ -928,6 +951,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const float* __restrict__ dL_ddepths, const float* __restrict__ dL_dalphas, float* __restrict__ contrib,
     uint8_t* __restrict__ written) {
     __shared__ float4 srec[64][4];
+    __shared__ float4 stage[64][3];
     const int lane = threadIdx.x & 63;
     const TileSched ts = tile_sched(sched - T, T);
     const uint32_t cnt = lane < 63 ? ts.bq_cnt[63 - lane] : 0u;
@@ -941,7 +965,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_
     const int tile = queue_tile(ts, T, blockIdx.x, pre, cnt);
     if (tile < 0) return;
     bwd_tile<4, false>(W, H, gx, tile, 0, (int)blockIdx.x, ranges, point_list, slot_vals, rec, bg, alphas, n_contrib,
-                       dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, srec, nullptr);
+                       dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, srec, nullptr, stage);
 }
 
 }  // namespace
