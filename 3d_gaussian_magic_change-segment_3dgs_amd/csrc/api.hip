@@ -330,6 +330,9 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
                           /*skip_sentinel=*/true);  // culled Gaussians (key ~0u) emit nothing
     }
     GSR_STAGE("depth sort");
+    // gsr_forward's speculative stage B with row binning computes the offsets and num_rendered
+    // in its level-1 kernels (binning_rows.hip, fused mode): no scan here
+    if (!wait && packed && g_rows_binning) return 0;
     {
         StageScope sc(GSR_STAGE_SCAN, st);
         if (packed)  // tile counts from the depth-ordered packed rects: no gather
@@ -400,7 +403,8 @@ int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* b
                                     at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.tkeys_alt),
                                     at<uint32_t>(b, BL.vals_alt), at<uint32_t>(b, BL.point_list),
                                     at<uint32_t>(b, BL.slot_vals), ranges, order, at<uint4>(b, BL.written),
-                                    cdiv(cap, 16), cap, n_total, st, stage);
+                                    cdiv(cap, 16), cap, n_total, st, stage, /*fused=*/true,
+                                    n_dev ? host_total_slot().dev : nullptr);
             };
             {
                 StageScope sc(GSR_STAGE_DUPLICATE, st);

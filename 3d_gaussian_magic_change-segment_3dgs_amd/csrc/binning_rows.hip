@@ -67,8 +67,11 @@ constexpr int RB_STAGE1 = 4 * RB_CH1;  // its row entries assembled in LDS (more
 #ifndef GSR_RB_CH
 #define GSR_RB_CH 512
 #endif
+// Level-2 grid: 768 blocks = three 512-thread blocks per CU on 256 CUs (k_tiles_scatter's LDS
+// allows three), one resident round grid-striding over the chunks (2048 blocks ran ~2.7 rounds
+// of block start-up: tile sort 0.0688 -> 0.0653 ms at the metric scene)
 #ifndef GSR_RB_GRID2
-#define GSR_RB_GRID2 2048
+#define GSR_RB_GRID2 768
 #endif
 constexpr int RB_CH = GSR_RB_CH;      // level 2: row entries per chunk = threads per block
 constexpr int RB_W = RB_CH / 32;      // bitmask words per bucket
@@ -157,25 +160,37 @@ __device__ __forceinline__ void unpack_rect(uint32_t pr, int& x0, int& y0, int& 
 
 // ---------------------------------------------------------------- level 1 --
 // table1[y * nch1 + c] = Gaussians of chunk c (RB_CH1 depth-ordered Gaussians) covering row y.
+// fused: table1[gy * nch1 + c] = the chunk's instances (sum of its Gaussians' tile counts), a row
+// after the others, so that the one scan of table1 also yields every chunk's first instance
+// slot (k_rows_scatter then computes the per-Gaussian offsets: no separate scan of the counts).
 __global__ void __launch_bounds__(RB_CH1) k_rows_count(int P, int gy, int nch1, const uint32_t* __restrict__ rect,
-                                                      uint32_t* __restrict__ table1, void* zero, size_t nzero16) {
+                                                      uint32_t* __restrict__ table1, void* zero, size_t nzero16,
+                                                      int fused) {
     __shared__ int d[RB_MAXB + 1];
     __shared__ uint32_t e[RB_MAXB + 1];
-    __shared__ uint32_t tot;
+    __shared__ uint32_t tot, s_inst;
     for (int i = threadIdx.x; i <= gy; i += RB_CH1) d[i] = 0;
+    if (threadIdx.x == 0) s_inst = 0;
     __syncthreads();
     const int r = blockIdx.x * RB_CH1 + threadIdx.x;
+    uint32_t ntile = 0;
     if (r < P) {
         int x0, y0, x1, y1;
         unpack_rect(rect[r], x0, y0, x1, y1);
         if (x1 > x0 && y1 > y0) {
             atomicAdd(&d[y0], 1);
             atomicAdd(&d[y1], -1);
+            ntile = (uint32_t)((x1 - x0) * (y1 - y0));
         }
+    }
+    if (fused) {
+        const uint32_t ws = (uint32_t)__builtin_amdgcn_readlane((int)scan_incl<64>(ntile), 63);
+        if ((threadIdx.x & 63) == 0 && ws) atomicAdd(&s_inst, ws);
     }
     __syncthreads();
     lds_scan256(reinterpret_cast<const uint32_t*>(d), gy + 1, e, &tot);  // e[y + 1] = rows' counts
     for (int y = threadIdx.x; y < gy; y += RB_CH1) table1[(size_t)y * nch1 + blockIdx.x] = e[y + 1];
+    if (fused && threadIdx.x == 0) table1[(size_t)gy * nch1 + blockIdx.x] = s_inst;
     // the scan's status words, cleared after the rect load (one in-order vmcnt for loads and stores)
     zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH1 + threadIdx.x, (size_t)gridDim.x * RB_CH1);
 }
@@ -186,31 +201,55 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_count(int P, int gy, int nch1, 
 // bound (gy = 68 at 1080p: 18 KB; 67 KB at gy = 255, covered by the 4080-px-tall case of
 // tests/test_gpu_parity.py::test_rows_binning_matches_radix_path).  Every global load is
 // issued before the first barrier.
+// fused (k_rows_count's extra table row): the Gaussians' instance offsets are computed here --
+// the chunk's first slot from the scanned table plus an exclusive block scan of the tile counts
+// -- and written to offsets (inclusive, as the scan of binning.hip writes them); the thread of
+// Gaussian P - 1 also stores num_rendered into host-mapped memory when host_total is given.
+// Otherwise the offsets are read (the depth-order scan ran).
 __global__ void __launch_bounds__(RB_CH1) k_rows_scatter(int P, int gy, int nch1, const uint32_t* __restrict__ order,
-                                                        const uint32_t* __restrict__ offsets,
+                                                        uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ rect,
                                                         const uint32_t* __restrict__ base1, uint32_t* __restrict__ goff,
                                                         uint32_t* __restrict__ e_gid, uint32_t* __restrict__ e_u,
-                                                        uint32_t* __restrict__ e_x, uint32_t cap) {
+                                                        uint32_t* __restrict__ e_x, uint32_t cap, int fused,
+                                                        uint32_t* host_total) {
     extern __shared__ uint32_t dyn[];
     uint32_t* bits = dyn;
     uint32_t* pre = dyn + gy * RB_S1;
     __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
     __shared__ uint32_t s_gid[RB_STAGE1], s_u[RB_STAGE1], s_x[RB_STAGE1];
     __shared__ uint32_t tot;
+    __shared__ uint32_t s_wsum[RB_CH1 / 64];
     BT_T(bt0)
     const int tid = threadIdx.x;
     const int r = blockIdx.x * RB_CH1 + tid;
     int x0 = 0, y0 = 0, x1 = 0, y1 = 0;
-    uint32_t g = 0, off = 0;
+    uint32_t g = 0, off = 0, cbase = 0;
     if (r < P) {
         unpack_rect(rect[r], x0, y0, x1, y1);
         g = order[r];
-        off = r == 0 ? 0u : offsets[r - 1];
+        if (!fused) off = r == 0 ? 0u : offsets[r - 1];
     }
+    if (fused) cbase = base1[(size_t)gy * nch1 + blockIdx.x] - base1[(size_t)gy * nch1];
     for (int i = tid; i < gy * RB_S1; i += RB_CH1) bits[i] = 0;
     for (int y = tid; y < gy; y += RB_CH1) gb[y] = base1[(size_t)y * nch1 + blockIdx.x];
+    const uint32_t ntile = (x1 > x0 && y1 > y0) ? (uint32_t)((x1 - x0) * (y1 - y0)) : 0u;
+    uint32_t incl = 0;
+    if (fused) {
+        incl = scan_incl<64>(ntile);
+        if ((tid & 63) == 63) s_wsum[tid >> 6] = incl;
+    }
     __syncthreads();
+    if (fused) {
+        uint32_t wpre = 0;
+        for (int w = 0; w < (tid >> 6); ++w) wpre += s_wsum[w];
+        off = cbase + wpre + incl - ntile;
+        if (r < P) {
+            offsets[r] = off + ntile;
+            if (r == P - 1 && host_total)
+                __hip_atomic_store(host_total, off + ntile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+    }
     const bool vis = x1 > x0 && y1 > y0;
     const uint32_t bit = 1u << (tid & 31), wd = (uint32_t)tid >> 5;
     if (vis)
@@ -498,7 +537,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
 }  // namespace
 
 size_t rows_bin_geom_ws_bytes(size_t P, int gy) {
-    const size_t n1 = (size_t)gy * cdiv(P > 0 ? P : 1, RB_CH1);
+    const size_t n1 = (size_t)(gy + 1) * cdiv(P > 0 ? P : 1, RB_CH1);  // + the fused mode's instance row
     return 2 * align_up(n1 * 4) + scan_ws_bytes(n1);
 }
 
@@ -507,17 +546,18 @@ size_t rows_bin_ws_bytes(size_t cap) {
     return ALIGN + align_up(TILE_BUCKET_WORDS * 4) + 2 * align_up(n2 * 4) + scan_ws_bytes(n2);
 }
 
-void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uint32_t* offsets, const uint32_t* rect,
+void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, uint32_t* offsets, const uint32_t* rect,
                          uint32_t* goff, void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_u, uint32_t* e_x,
                          uint32_t* point_list, uint32_t* slot_vals, uint2* ranges, uint32_t* tile_order,
                          uint4* written, size_t written16, size_t cap, const uint32_t* n_total, hipStream_t st,
-                         int stage) {
+                         int stage, bool fused, uint32_t* host_total) {
     const int nch1 = (int)cdiv(P, RB_CH1);
-    const size_t n1 = (size_t)gy * nch1;
+    const size_t n1a = (size_t)(gy + 1) * nch1;              // table rows (+ the fused mode's instance row)
+    const size_t n1 = (size_t)(gy + (fused ? 1 : 0)) * nch1;  // entries scanned
     char* gw = static_cast<char*>(geom_ws);
     uint32_t* table1 = reinterpret_cast<uint32_t*>(gw);
-    uint32_t* base1 = reinterpret_cast<uint32_t*>(gw + align_up(n1 * 4));
-    void* scan1 = gw + 2 * align_up(n1 * 4);
+    uint32_t* base1 = reinterpret_cast<uint32_t*>(gw + align_up(n1a * 4));
+    void* scan1 = gw + 2 * align_up(n1a * 4);
     const ScanWs S1 = scan_ws(n1, scan1);
     const size_t n2 = (size_t)gx * (gy + cdiv(cap, RB_CH));  // table-2 entries bound
     char* bw = static_cast<char*>(bin_ws);
@@ -531,10 +571,10 @@ void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uin
     const uint32_t cap32 = (uint32_t)(cap < 0xFFFFFFFFull ? cap : 0xFFFFFFFFull);
     if (stage == 0) {  // level 1: rows
         hipLaunchKernelGGL(k_rows_count, dim3(nch1), dim3(RB_CH1), 0, st, P, gy, nch1, rect, table1, S1.base,
-                           cdiv(S1.bytes, 16));
+                           cdiv(S1.bytes, 16), (int)fused);
         launch_scan_exclusive(table1, base1, n1, nullptr, S1, st);
         hipLaunchKernelGGL(k_rows_scatter, dim3(nch1), dim3(RB_CH1), 2 * gy * RB_S1 * 4, st, P, gy, nch1, order,
-                           offsets, rect, base1, goff, e_gid, e_u, e_x, cap32);
+                           offsets, rect, base1, goff, e_gid, e_u, e_x, cap32, (int)fused, host_total);
     } else if (stage == 1) {  // level 2: tiles (+ ranges)
         const int grid2 = (int)std::min<size_t>(RB_GRID2, gy + cdiv(cap, RB_CH));
         hipLaunchKernelGGL(k_tiles_count, dim3(grid2), dim3(RB_CH), 0, st, gx, gy, nch1, table1, base1, e_x, table2,

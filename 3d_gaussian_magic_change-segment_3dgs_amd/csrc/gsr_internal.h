@@ -315,11 +315,14 @@ void launch_scan_exclusive(const uint32_t* src, uint32_t* out, size_t n, const u
 // stage 0: level 1 (rows, goff); 1: level 2 (point_list, slot_vals, written flags
 // cleared); 2: ranges + heavy-first tile order.  geom_ws: rows_bin_geom_ws_bytes(P, gy)
 // bytes (the depth sort's workspace, free by then); bin_ws: rows_bin_ws_bytes(cap).
-void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, const uint32_t* offsets, const uint32_t* rect,
+// fused: level 1 also computes the depth-ordered instance offsets (written to offsets, as the
+// depth-order scan writes them; num_rendered also to host_total when non-NULL), so the scan need
+// not run first.
+void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, uint32_t* offsets, const uint32_t* rect,
                          uint32_t* goff, void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_u, uint32_t* e_x,
                          uint32_t* point_list, uint32_t* slot_vals, uint2* ranges, uint32_t* tile_order,
                          uint4* written, size_t written16, size_t cap, const uint32_t* n_total, hipStream_t st,
-                         int stage);
+                         int stage, bool fused, uint32_t* host_total);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, const uint32_t* rect_sorted, int gx, uint32_t* tkeys,
                       uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, uint32_t cap, hipStream_t st);

@@ -403,6 +403,7 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
                 live[kk] &= ~m_done;
                 const bool ok = __builtin_amdgcn_inverse_ballot_w64(m_o & ~m_done);
                 STAT(4, POPC(ok));
+                STAT(10, POPC(ok) == 0);
                 const float aT = (ok ? alpha : 0.f) * T[kk];
                 C0[kk] = __builtin_fmaf(cr, aT, C0[kk]);
                 C1[kk] = __builtin_fmaf(cg, aT, C1[kk]);
@@ -769,6 +770,9 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                 STAT(3, 1);
                 const float4 q2 = srec[j][2], q3 = srec[j][3];
                 const float op = q1.z, dep = q3.x, s0v = q1.w;
+#ifdef GSR_STATS
+                unsigned long long okst_ = st_[12];
+#endif
                 const float c0 = q2.x, c1 = q2.y, c2 = q2.z, s1v = q2.w;
                 float acc[12];
 #pragma unroll
@@ -786,6 +790,8 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                         near[k] & __builtin_amdgcn_ballot_w64(power[k] <= 0.0f) &
                         __builtin_amdgcn_ballot_w64(a >= ALPHA_MIN));
                     STAT(4, POPC(o));
+                    STAT(10, POPC(o) == 0);
+                    STAT(12, POPC(o) > 0);
                     // a_m = alpha of a replayed pair, else 0: it masks dch and the Dk fold, and
                     // makes Tn == T exactly off o (T / 1), so T needs no select; off o, a itself
                     // may be anything (-inf * 0 would poison the quotient's correction step)
@@ -841,6 +847,9 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                     acc[7] = __builtin_fmaf(ca, qx, cb * qy);
                     acc[8] = __builtin_fmaf(cc, qy, cb * qx);
                 }
+#endif
+#ifdef GSR_STATS
+                STAT(11, st_[12] == okst_);
 #endif
                 int vidx;
                 bool valid;

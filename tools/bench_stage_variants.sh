@@ -12,5 +12,5 @@ for so in "" build/variants/libgsr_*.so; do
     > gpurun_out/bs.json 2> gpurun_out/bs.err || { echo "$name failed"; tail -5 gpurun_out/bs.err; exit 1; }
   echo "== $name $(python -c "
 import json,sys;d=json.load(open('gpurun_out/bs.json'))
-print(d['value'], ' '.join('%s=%.4f' % (s, d['stages'][s]['avg_ms']) for s in sys.argv[1:]))" $stages)"
+print(d['value'], ' '.join('%s=%.4f' % (s, d['stages'].get(s, {}).get('avg_ms', 0.0)) for s in sys.argv[1:]))" $stages)"
 done

@@ -38,6 +38,8 @@ def main():
               f"near_skip={ns} ({ns / max(it, 1):.1%}) full={full} strips={strips} ({strips / max(full, 1):.2f}/full) "
               f"ok_px={okpx} lane_eff={okpx / max(64 * strips, 1):.1%}")
     print(f"bwd batches with a lane whose replay starts inside the batch: {s[16 + 9]} of {s[16 + 5]}")
+    print(f"fwd blended quadrants without a contributing pixel: {s[10]} of {s[8]}; bwd replayed strips without one: "
+          f"{s[16 + 10]} of {s[16 + 8]}; bwd records whose replayed strips had none: {s[16 + 11]} of {s[16 + 3]}")
 
 
 if __name__ == "__main__":
