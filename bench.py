@@ -346,14 +346,19 @@ def main():
 
     step = make_step(B)
 
-    def timed(fn, k, per_step=None):
+    def timed(fn, k, per_step=None, stride=1, dom_mask=0):
         """k steps between a barrier + device sync on both sides; max over ranks.  Python's
         cyclic GC is paused (collected before the untimed stage pass that precedes this, not
         here: a collection while the GPU sits idle before the timed region let the clocks
         drop, and the first five timed steps ran 10-28% slow; a collection inside the loop
         stalls the host behind the per-view num_rendered sync).  per_step (a list) receives
-        each step's duration from events recorded on the compute stream between the steps."""
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(k + 1)] if per_step is not None else None
+        the mean step duration of every window of `stride` steps, from events recorded on the
+        compute stream between the windows; the dominant stage's event bracket (dom_mask) is
+        armed on the first step of each window.  An event costs the stream a few microseconds
+        (the kernel trace showed ~5 us before the next kernel starts), so both are sampled
+        once per window rather than every step."""
+        nw = k // stride
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(nw + 1)] if per_step is not None else None
         gc.disable()
         if dist is not None:
             dist.barrier()
@@ -362,9 +367,11 @@ def main():
         if evs:
             evs[0].record()
         for i in range(k):
+            if dom_mask:
+                _C._lib.gsr_timing_enable(dom_mask if i % stride == 0 else 0)
             fn()
-            if evs:
-                evs[i + 1].record()
+            if evs and (i + 1) % stride == 0 and (i + 1) // stride <= nw:
+                evs[(i + 1) // stride].record()
         drain()
         torch.cuda.synchronize()
         gc.enable()
@@ -372,7 +379,7 @@ def main():
             dist.barrier()
         el = time.perf_counter() - t_start
         if evs:
-            per_step.extend(evs[i].elapsed_time(evs[i + 1]) for i in range(k))
+            per_step.extend(evs[w].elapsed_time(evs[w + 1]) / stride for w in range(nw))
         if dist is not None:
             t = torch.tensor([el], device=device, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -408,9 +415,9 @@ def main():
     _C._lib.gsr_timing_enable(0)
     sms, scnt = collect()
     dom_i = max(range(nst), key=lambda i: sms[i]) if any(scnt) else 0
-    _C._lib.gsr_timing_enable(1 << dom_i)
     step_ms = []
-    elapsed = timed(step, args.steps, step_ms)
+    stride = 4 if args.steps >= 8 else 1
+    elapsed = timed(step, args.steps, step_ms, stride=stride, dom_mask=1 << dom_i)
     _C._lib.gsr_timing_enable(0)
     ms, cnt = collect()  # the dominant stage's launches inside the timed region
     I, HW = int(state["I"]), W * H
@@ -465,7 +472,8 @@ def main():
                      "max": round(max(step_ms), 4),
                      "slowest": [(i, round(t, 3)) for t, i in sorted(((t, i) for i, t in enumerate(step_ms)),
                                                                     reverse=True)[:5]],
-                     "source": "hipEvents between steps on the compute stream (rank 0)"} if step_ms else None),
+                     "source": f"hipEvents on the compute stream every {stride} steps, per-step means of "
+                               f"those windows (rank 0)"} if step_ms else None),
         "vs_baseline": None, "dtype": "f32", "data": "synthetic (SURVEY.md s8d generator, seed 0; upstream grads "
                                                     "N(0,1)*1e-3 seed 1)",
         "config": {"workload": f"{args.config}: P={P} Gaussians, SH{deg}, {W}x{H}, fwd+bwd per view; {B} view(s) per "
