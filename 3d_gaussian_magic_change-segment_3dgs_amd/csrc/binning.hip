@@ -909,29 +909,47 @@ __global__ void __launch_bounds__(ORDER_THREADS) k_tile_order(uint2* __restrict_
 }
 
 // The same schedule when the non-empty buckets were counted upstream (row binning:
-// k_tiles_scatter adds each row's bucket counts into bw[0, 33)): one thread per tile over
+// k_tiles_scatter adds each row's fine-bucket counts into bw[0, 132)): one thread per tile over
 // many blocks instead of one block walking every tile twice (11-12 us at 8160 tiles,
-// latency-bound on one CU).  A wave's lanes that share a bucket are grouped by a 6-ballot
-// match and take one global atomic position per group (bw[64 + b]).  Empty tiles (bucket
-// 0, including rows the binning never visited) go last, so their count is not needed.
+// latency-bound on one CU).  Fine buckets (quarter octaves of the list length, len_fbucket):
+// inside one octave the lengths differ up to 2x, and the dispatcher then hands out tiles of
+// very different work in arbitrary order.  A wave's lanes that share a bucket are grouped by an
+// 8-ballot match and take one global atomic position per group (bw[TILE_BUCKET_POS + b]).
+// Empty tiles (bucket 0, including rows the binning never visited) go last, so their count is
+// not needed.
 __global__ void __launch_bounds__(256) k_tile_order_counted(const uint2* __restrict__ ranges, int T,
                                                             uint32_t* bw, uint32_t* __restrict__ order,
                                                             int split_fwd) {
-    __shared__ uint32_t boff[33];
+    __shared__ uint32_t boff[FINE_BUCKETS];
     const int tid = threadIdx.x;
-    if (tid < 64) {  // heavy first: exclusive offsets over buckets 32, 31, ..., 1; then bucket 0
-        const uint32_t v = tid < 32 ? bw[32 - tid] : 0u;
-        uint32_t x = v;
+    if (tid < 64) {  // heavy first: exclusive offsets over buckets 131, 130, ..., 1; then bucket 0
+        // lane l: heavy-order positions 3l .. 3l + 2 = buckets 131 - 3l - i
+        uint32_t v[3], s = 0;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int b = FINE_BUCKETS - 1 - (3 * tid + i);
+            v[i] = b >= 1 ? bw[b] : 0u;
+            s += v[i];
+        }
+        uint32_t x = s;
 #pragma unroll
         for (int o = 1; o < 64; o <<= 1) {
             const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
             if (tid >= o) x += y;
         }
-        if (tid < 32) boff[32 - tid] = x - v;
-        if (tid == 31) boff[0] = x;
+        uint32_t e = x - s;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            const int b = FINE_BUCKETS - 1 - (3 * tid + i);
+            if (b >= 1) boff[b] = e;
+            e += v[i];
+        }
+        if (tid == 63) boff[0] = x;  // every non-empty tile comes first
     }
     __syncthreads();
-    if (blockIdx.x == 0 && tid == 0) write_sched(order + T, boff, split_fwd);
+    // forward split: tiles with n >= 2^(B-1) = fine buckets >= 4B
+    if (blockIdx.x == 0 && tid == 0)
+        order[T + SCHED_FWD_SPLIT] = split_fwd > 0 && 4 * split_fwd <= FINE_BUCKETS ? boff[4 * split_fwd - 1] : 0u;
     {  // the forward's backward queue starts empty
         const TileSched ts = tile_sched(order, T);
         if (blockIdx.x == 0 && tid < BQ_BUCKETS) ts.bq_cnt[tid] = 0u;
@@ -940,17 +958,17 @@ __global__ void __launch_bounds__(256) k_tile_order_counted(const uint2* __restr
     }
     const int t = blockIdx.x * 256 + tid;
     const bool valid = t < T;
-    const uint32_t b = valid ? len_bucket(ranges[t]) : 0u;
+    const uint32_t b = valid ? len_fbucket(ranges[t]) : 0u;
     uint64_t peers = __ballot(valid);
 #pragma unroll
-    for (int k = 0; k < 6; ++k) {  // buckets 0..32
+    for (int k = 0; k < 8; ++k) {  // buckets 0..131
         const bool set = (b >> k) & 1u;
         const uint64_t m = __ballot(set);
         peers &= set ? m : ~m;
     }
     const uint64_t lt = lanemask_lt();
     uint32_t base = 0;
-    if (valid && (peers & lt) == 0) base = atomicAdd(&bw[64 + b], (uint32_t)__popcll(peers));
+    if (valid && (peers & lt) == 0) base = atomicAdd(&bw[TILE_BUCKET_POS + b], (uint32_t)__popcll(peers));
     const int leader = valid ? (int)__builtin_ctzll(peers) : 0;
     base = (uint32_t)__shfl((int)base, leader, 64);
     if (valid) order[boff[b] + base + (uint32_t)__popcll(peers & lt)] = (uint32_t)t;

@@ -423,7 +423,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
     __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
     __shared__ uint32_t s_gid[RB_STAGE], s_u[RB_STAGE], s_gp[RB_STAGE];
     __shared__ uint32_t tot;
-    __shared__ uint32_t s_bc[33];  // this row's tiles per schedule bucket (k_tile_order_counted)
+    __shared__ uint32_t s_bc[FINE_BUCKETS];  // this row's tiles per fine schedule bucket (k_tile_order_counted)
     BT_T(bt0)
     const int tid = threadIdx.x;
     build_row_map(m, gy, nch1, table1, base1, cap);
@@ -458,7 +458,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
         const int y = cur.y;
         for (int i = tid; i < gx * RB_S; i += RB_CH) bits[i] = 0;
         if (tid < gx) gb[tid] = cur.gbv;
-        if (tid < 33) s_bc[tid] = 0;
+        if (tid < FINE_BUCKETS) s_bc[tid] = 0;
         __syncthreads();
         const bool live = (uint32_t)tid < cur.n;
         const int x0 = (int)(cur.xr & 255u), x1 = (int)((cur.xr >> 8) & 255u);
@@ -476,14 +476,14 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
             b = min(b, cap);
             const uint2 rg = b > a ? make_uint2(a, b) : make_uint2(0u, 0u);
             ranges[(size_t)y * gx + tid] = rg;
-            const uint32_t bk = len_bucket(rg);
+            const uint32_t bk = len_fbucket(rg);
             if (bk) atomicAdd(&s_bc[bk], 1u);
         }
         const uint32_t cn = c + gridDim.x;
         Chunk nxt{};
         if (cn < m.nch2) nxt = fetch(cn);  // in flight while this chunk is ranked
         __syncthreads();
-        if (cur.s == 0 && tid < 33 && s_bc[tid]) atomicAdd(&bucket_words[tid], s_bc[tid]);
+        if (cur.s == 0 && tid < FINE_BUCKETS && s_bc[tid]) atomicAdd(&bucket_words[tid], s_bc[tid]);
         bucket_prefix<RB_CH>(bits, gx, pre, cnt);
         lds_scan256(cnt, gx, lst, &tot);
         const bool staged = tot <= (uint32_t)RB_STAGE;  // uniform

@@ -50,9 +50,19 @@ __device__ __forceinline__ uint32_t len_bucket(uint2 r) {
     const uint32_t len = r.y - r.x;
     return len ? 32 - __clz(len) : 0;
 }
-// Bucket-count words of the row binning's tile order (k_tiles_scatter counts the non-empty
-// buckets, k_tile_order_counted ranks the tiles): counts at [0, 33), positions at [64, 97).
-constexpr int TILE_BUCKET_WORDS = 128;
+// Finer schedule bucket of the row-binning path: quarter octaves, 4 * bit length + the two bits
+// below the leading one (0 = empty, up to 131).  Bit length B <-> fine buckets [4B, 4B + 3].
+constexpr int FINE_BUCKETS = 132;
+__device__ __forceinline__ uint32_t len_fbucket(uint2 r) {
+    const uint32_t len = r.y - r.x;
+    if (!len) return 0;
+    const uint32_t bl = 32 - __clz(len);
+    const uint32_t sub = bl >= 3 ? (len >> (bl - 3)) & 3u : (len << (3 - bl)) & 3u;
+    return 4 * bl + sub;
+}
+// Bucket-count words of the row binning's tile order (k_tiles_scatter counts the non-empty fine
+// buckets, k_tile_order_counted ranks the tiles): counts at [0, 132), positions at [256, 388).
+constexpr int TILE_BUCKET_WORDS = 512, TILE_BUCKET_POS = 256;
 __device__ __forceinline__ void zero16(void* p, size_t n4, size_t tid, size_t nthreads) {
     uint4* q = static_cast<uint4*>(p);
     for (size_t i = tid; i < n4; i += nthreads) q[i] = make_uint4(0u, 0u, 0u, 0u);
