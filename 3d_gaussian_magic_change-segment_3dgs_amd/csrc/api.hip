@@ -237,6 +237,10 @@ int gsr_set_option(const char* name, long long value) {
         gsr::set_split_buckets((int)value, gsr::split_bwd_depth());
         return 0;
     }
+    if (std::string(name) == "split4_fwd_bucket") {  // render forward: tiles with n >= 2^(v-1) on four waves; 0 = off
+        gsr::set_split4_bucket((int)value);
+        return 0;
+    }
     if (std::string(name) == "split_bwd_depth") {  // render backward: tiles this deep on two waves; 0 = off
         gsr::set_split_buckets(gsr::split_fwd_bucket(), (int)value);
         return 0;

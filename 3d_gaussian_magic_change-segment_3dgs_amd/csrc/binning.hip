@@ -854,11 +854,13 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
 constexpr int ORDER_THREADS = 1024, ORDER_WAVES = ORDER_THREADS / 64;
 // sched[SCHED_*] = tiles in length buckets >= the kernel's split bucket B (the heavy-first
 // order lists buckets 32, 31, ..., so that is bucket B - 1's offset); B = 0: no split.
-__device__ __forceinline__ void write_sched(uint32_t* sched, const uint32_t* boff, int split_fwd) {
+__device__ __forceinline__ void write_sched(uint32_t* sched, const uint32_t* boff, int split_fwd, int split4_fwd) {
     sched[SCHED_FWD_SPLIT] = split_fwd > 0 && split_fwd <= 33 ? boff[split_fwd - 1] : 0u;
+    sched[SCHED_FWD_QUARTER] = split4_fwd > 0 && split4_fwd <= 33 ? boff[split4_fwd - 1] : 0u;
 }
 __global__ void __launch_bounds__(ORDER_THREADS) k_tile_order(uint2* __restrict__ ranges, int T,
-                                                              uint32_t* __restrict__ order, int split_fwd) {
+                                                              uint32_t* __restrict__ order, int split_fwd,
+                                                              int split4_fwd) {
     __shared__ uint32_t wcnt[ORDER_WAVES][33];
     const int tid = threadIdx.x, wave = tid >> 6;
     for (int i = tid; i < ORDER_WAVES * 33; i += ORDER_THREADS) (&wcnt[0][0])[i] = 0;
@@ -900,7 +902,7 @@ __global__ void __launch_bounds__(ORDER_THREADS) k_tile_order(uint2* __restrict_
         if (tid < 33) boff[32 - tid] = x - v;
     }
     __syncthreads();
-    if (tid == 0) write_sched(order + T, boff, split_fwd);
+    if (tid == 0) write_sched(order + T, boff, split_fwd, split4_fwd);
 #pragma unroll 4
     for (int t = tid; t < T; t += ORDER_THREADS) {
         const uint32_t b = len_bucket(ranges[t]);
@@ -919,7 +921,7 @@ __global__ void __launch_bounds__(ORDER_THREADS) k_tile_order(uint2* __restrict_
 // not needed.
 __global__ void __launch_bounds__(256) k_tile_order_counted(const uint2* __restrict__ ranges, int T,
                                                             uint32_t* bw, uint32_t* __restrict__ order,
-                                                            int split_fwd) {
+                                                            int split_fwd, int split4_fwd) {
     __shared__ uint32_t boff[FINE_BUCKETS];
     const int tid = threadIdx.x;
     if (tid < 64) {  // heavy first: exclusive offsets over buckets 131, 130, ..., 1; then bucket 0
@@ -948,8 +950,11 @@ __global__ void __launch_bounds__(256) k_tile_order_counted(const uint2* __restr
     }
     __syncthreads();
     // forward split: tiles with n >= 2^(B-1) = fine buckets >= 4B
-    if (blockIdx.x == 0 && tid == 0)
+    if (blockIdx.x == 0 && tid == 0) {
         order[T + SCHED_FWD_SPLIT] = split_fwd > 0 && 4 * split_fwd <= FINE_BUCKETS ? boff[4 * split_fwd - 1] : 0u;
+        order[T + SCHED_FWD_QUARTER] =
+            split4_fwd > 0 && 4 * split4_fwd <= FINE_BUCKETS ? boff[4 * split4_fwd - 1] : 0u;
+    }
     {  // the forward's backward queue starts empty
         const TileSched ts = tile_sched(order, T);
         if (blockIdx.x == 0 && tid < BQ_BUCKETS) ts.bq_cnt[tid] = 0u;
@@ -1134,7 +1139,12 @@ void launch_scan_exclusive(const uint32_t* src, uint32_t* out, size_t n, const u
 #ifndef GSR_SPLIT_BWD_DEPTH
 #define GSR_SPLIT_BWD_DEPTH 0
 #endif
-static int g_split_fwd = GSR_SPLIT_FWD, g_split_bwd_depth = GSR_SPLIT_BWD_DEPTH;
+#ifndef GSR_SPLIT4_FWD
+#define GSR_SPLIT4_FWD 0
+#endif
+static int g_split_fwd = GSR_SPLIT_FWD, g_split_bwd_depth = GSR_SPLIT_BWD_DEPTH, g_split4_fwd = GSR_SPLIT4_FWD;
+void set_split4_bucket(int b) { g_split4_fwd = b >= 0 ? b : GSR_SPLIT4_FWD; }
+int split4_fwd_bucket() { return g_split4_fwd; }
 void set_split_buckets(int fwd_bucket, int bwd_depth) {
     g_split_fwd = fwd_bucket >= 0 ? fwd_bucket : GSR_SPLIT_FWD;
     g_split_bwd_depth = bwd_depth >= 0 ? bwd_depth : GSR_SPLIT_BWD_DEPTH;
@@ -1146,12 +1156,12 @@ void launch_tile_order_counted(const uint2* ranges, int T, uint32_t* bucket_word
                                hipStream_t st) {
     if (T == 0) return;
     hipLaunchKernelGGL(k_tile_order_counted, dim3((unsigned)cdiv((size_t)T, 256)), dim3(256), 0, st, ranges, T,
-                       bucket_words, order, g_split_fwd);
+                       bucket_words, order, g_split_fwd, g_split4_fwd);
 }
 
 void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st) {
     if (T == 0) return;
-    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ranges, T, order, g_split_fwd);
+    hipLaunchKernelGGL(k_tile_order, dim3(1), dim3(1024), 0, st, ranges, T, order, g_split_fwd, g_split4_fwd);
 }
 
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,

@@ -197,7 +197,7 @@ inline size_t scratch_bytes(size_t I) { return align_up(I * 12 * sizeof(float)) 
 //                       deepest first;
 //   tdone[T]:           split forward tiles: sum over finished halves of (depth << 1) | 1.
 // bq_cnt and tdone are zeroed by the tile-order kernels.
-constexpr int SCHED_FWD_SPLIT = 0, SCHED_WORDS = 4;
+constexpr int SCHED_FWD_SPLIT = 0, SCHED_FWD_QUARTER = 1, SCHED_WORDS = 4;
 constexpr int BQ_BUCKETS = 64, BQ_STEP = 16;
 struct TileSched {
     uint32_t *sched, *bq_cnt, *tdone, *bq_list;
@@ -308,6 +308,9 @@ void set_sort_grouped(bool on);  // grouped look-back passes for sorts of <= 256
 // the backward queue's counters (TileSched).  bwd_depth: the backward splits tiles whose
 // deepest contributor is at least this deep (0 = no split; a render.hip launch argument).
 void set_split_buckets(int fwd_bucket, int bwd_depth);  // negative: the built-in default
+// forward quarter tiles: tiles with n >= 2^(B-1) get four waves (0 = off; negative: default)
+void set_split4_bucket(int fwd_bucket);
+int split4_fwd_bucket();
 int split_bwd_depth();
 int split_fwd_bucket();
 void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st);

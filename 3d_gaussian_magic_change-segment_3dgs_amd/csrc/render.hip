@@ -228,11 +228,22 @@ __device__ __forceinline__ bool tile_hit(float x, float y, float a, float b, flo
 // own add returned -- one relaxed atomic, no fences (an acquire / release pair costs an
 // L2 write-back + invalidate on this multi-XCD part: the split forward ran 50% slower
 // with it).  Lane 0 only.
-__device__ __forceinline__ void publish_depth(const TileSched& ts, int T, int tile, bool half, uint32_t d) {
-    if (half) {
+// Quarter tiles (4 parts): the word holds (max depth << 2) | parts done, updated by a
+// compare-and-swap loop; the part that completes the count files the tile.
+__device__ __forceinline__ void publish_depth(const TileSched& ts, int T, int tile, int parts, uint32_t d) {
+    if (parts == 2) {
         const uint32_t old = atomicAdd(&ts.tdone[tile], (d << 1) | 1u);
         if (!(old & 1u)) return;  // first half: the second files the tile
         d = max(d, old >> 1);
+    } else if (parts == 4) {
+        uint32_t old = ts.tdone[tile], assumed;
+        do {
+            assumed = old;
+            const uint32_t nv = (max(assumed >> 2, d) << 2) | ((assumed & 3u) + 1u);
+            old = atomicCAS(&ts.tdone[tile], assumed, nv);
+        } while (old != assumed);
+        if ((old & 3u) != 3u) return;  // not the last quarter
+        d = max(d, old >> 2);
     }
     const uint32_t b = depth_bucket(d);
     if (b == 0) return;  // nothing for the backward to replay
@@ -254,16 +265,20 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
     // colour/depth/segment sums, which nothing amplifies, use explicit FMAs.
 #pragma clang fp contract(off)
     WT_BEGIN
-    constexpr int NR = NQ / 2;  // quadrant rows covered: 2 (whole tile) or 1 (half)
+    // quadrant rows / columns covered: 2 x 2 (whole tile), 1 x 2 (half), 1 x 1 (quarter)
+    constexpr int NR = NQ == 4 ? 2 : 1, NC = NQ == 1 ? 1 : 2;
     const int lane = threadIdx.x & 63;
     const int tx = tile % gx, ty = tile / gx;
-    const int r0 = q0 >> 1;     // first quadrant row
+    const int r0 = q0 >> 1;                    // first quadrant row
+    const int c0 = NQ == 1 ? (q0 & 1) : 0;     // first quadrant column
     // Lane l owns pixel (l & 7, l >> 3) of each 8x8 quadrant k of the tile (k & 1: right
     // half, k >> 1: bottom half).  Square quadrants are gated tighter than 16x4 strips:
     // 8.7% fewer (quadrant, Gaussian) blends at the metric scene (tools/render_stats.py).
-    // Quadrant kk of this wave is k = q0 + kk: column kk & 1, row r0 + (kk >> 1).
+    // Quadrant kk of this wave is k = q0 + kk: column c0 + kk % NC, row r0 + kk / NC.
     const int px0 = tx * BX + (lane & 7), py0 = ty * BY + (lane >> 3);
-    const float pfx[2] = {(float)px0, (float)(px0 + 8)};
+    float pfx[NC];
+#pragma unroll
+    for (int cc = 0; cc < NC; ++cc) pfx[cc] = (float)(px0 + 8 * (c0 + cc));
     float pfy[NR];
 #pragma unroll
     for (int rr = 0; rr < NR; ++rr) pfy[rr] = (float)(py0 + 8 * (r0 + rr));
@@ -287,8 +302,8 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
     STAT_DECL
     STAT(7, n);
     // prefilter rectangle: the pixels this wave owns
-    const float x0 = (float)(tx * BX), y0 = (float)(ty * BY + 8 * r0);
-    const float x1 = (float)min(tx * BX + BX - 1, W - 1), y1 = (float)min(ty * BY + 8 * (r0 + NR) - 1, H - 1);
+    const float x0 = (float)(tx * BX + 8 * c0), y0 = (float)(ty * BY + 8 * r0);
+    const float x1 = (float)min(tx * BX + 8 * (c0 + NC) - 1, W - 1), y1 = (float)min(ty * BY + 8 * (r0 + NR) - 1, H - 1);
 
     // Two-stage software pipeline over batches of 64 instances: while batch b is
     // blended, the records of batch b+1 and the ids of batch b+2 are in flight
@@ -325,8 +340,8 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
                 if (kk & 1) cr |= live[kk]; else cl |= live[kk];
                 if (kk >> 1) rbm |= live[kk]; else rt |= live[kk];
             }
-            if (!cl) lx0 = x0 + 8.f;
-            if (!cr) lx1 = fminf(x1, x0 + 7.f);
+            if (NC == 2 && !cl) lx0 = x0 + 8.f;
+            if (NC == 2 && !cr) lx1 = fminf(x1, x0 + 7.f);
             if (NR == 2 && !rt) ly0 = y0 + 8.f;
             if (NR == 2 && !rbm) ly1 = fminf(y1, y0 + 7.f);
         }
@@ -348,8 +363,13 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
             const float gx_ = q0v.x, gy_ = q0v.y, ca = q0v.z, cb = q0v.w, cc = q1v.x, pm = q1v.y;
             // power = -0.5 (a dx dx + c dy dy) - b dx dy, rounded as forward.cu:349 writes
             // it; the products are shared by the quadrants of a column / row.
-            const float dx0 = gx_ - pfx[0], dx1 = gx_ - pfx[1];
-            const float ax[2] = {ca * dx0 * dx0, ca * dx1 * dx1}, bx[2] = {cb * dx0, cb * dx1};
+            float ax[NC], bx[NC];
+#pragma unroll
+            for (int cc = 0; cc < NC; ++cc) {
+                const float dxc = gx_ - pfx[cc];
+                ax[cc] = ca * dxc * dxc;
+                bx[cc] = cb * dxc;
+            }
             float cy[NR], dyv[NR];
 #pragma unroll
             for (int rr = 0; rr < NR; ++rr) {
@@ -370,7 +390,7 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
                 }
 #endif
                 // -0.5 S is exact, so -(0.5 S) - B as one fma(-0.5, S, -B): the same bits
-                power[kk] = __builtin_fmaf(-0.5f, ax[kk & 1] + cy[kk >> 1], -(bx[kk & 1] * dyv[kk >> 1]));
+                power[kk] = __builtin_fmaf(-0.5f, ax[kk % NC] + cy[kk / NC], -(bx[kk % NC] * dyv[kk / NC]));
                 near[kk] = __builtin_amdgcn_ballot_w64(power[kk] >= pm) & live[kk];
                 any_near |= near[kk];
             }
@@ -423,7 +443,7 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
     for (int kk = 0; kk < NQ; ++kk) deepest = max(deepest, last[kk]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) deepest = max(deepest, (uint32_t)__shfl_xor((int)deepest, o, 64));
-    if (lane == 0) publish_depth(ts, ntiles, tile, NQ != 4, deepest);
+    if (lane == 0) publish_depth(ts, ntiles, tile, 4 / NQ, deepest);
     WT_END(0, wslot, tile, n, deepest, NQ)
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
     const size_t HW = (size_t)H * W;
@@ -444,9 +464,14 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
     }
 }
 
-// Block b < 2 Hs: half (b & 1) of heavy tile order[b >> 1] (the first Hs entries of the
-// heavy-first schedule, sched[0], written by the tile-order kernel); then one wave per
-// remaining tile.  The grid is sized for Hs = T; blocks past the work return at once.
+// Block b < 4 Qs: quadrant (b & 3) of the heaviest tile order[b >> 2] (the first Qs entries
+// of the heavy-first schedule, sched[SCHED_FWD_QUARTER]); then, up to Hs (sched[SCHED_FWD_SPLIT],
+// Hs >= Qs), half (b & 1) of the next heavy tiles; then one wave per remaining tile.  The grid is
+// sized for the worst case; blocks past the work return at once.  Quarter waves (option
+// split4_fwd_bucket, off by default) measured slower at every threshold (metric scene, render_fwd
+// 0.206 ms without; n >= 2048: 0.222, >= 1024: 0.233, >= 512: 0.246, >= 256: 0.241): each quarter
+// wave repeats the batch loads, the prefilter and the per-instance record reads and ballots for
+// one 8x8 quadrant (profiles/round3_quarter_sweep.txt).
 __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, int T, const uint32_t* __restrict__ order,
                                                    uint32_t* __restrict__ sched,
                                                    const uint2* __restrict__ ranges,
@@ -458,12 +483,17 @@ __global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, int T, 
     __shared__ float4 srec[64][4];
     const TileSched ts = tile_sched(sched - T, T);
     const uint32_t Hs = min(sched[SCHED_FWD_SPLIT], (uint32_t)T);
+    const uint32_t Qs = min(sched[SCHED_FWD_QUARTER], Hs);
     const uint32_t b = blockIdx.x;
-    if (b < 2 * Hs) {
-        fwd_tile<2>(W, H, gx, T, (int)order[b >> 1], 2 * (int)(b & 1), (int)b, ts, ranges, point_list, rec, bg,
+    if (b < 4 * Qs) {
+        fwd_tile<1>(W, H, gx, T, (int)order[b >> 2], (int)(b & 3), (int)b, ts, ranges, point_list, rec, bg,
                     out_color, out_depth, out_alpha, out_segment, n_contrib, srec);
+    } else if (b < 4 * Qs + 2 * (Hs - Qs)) {
+        const uint32_t h = b - 4 * Qs;
+        fwd_tile<2>(W, H, gx, T, (int)order[Qs + (h >> 1)], 2 * (int)(h & 1), (int)b, ts, ranges, point_list, rec,
+                    bg, out_color, out_depth, out_alpha, out_segment, n_contrib, srec);
     } else {
-        const uint32_t i = b - Hs;
+        const uint32_t i = b - 2 * Qs - Hs;  // = Hs + (b - 4 Qs - 2 (Hs - Qs))
         if (i >= (uint32_t)T) return;
         fwd_tile<4>(W, H, gx, T, (int)order[i], 0, (int)b, ts, ranges, point_list, rec, bg, out_color, out_depth,
                     out_alpha, out_segment, n_contrib, srec);
@@ -985,7 +1015,9 @@ void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, 
                            uint32_t* n_contrib, hipStream_t st) {
     const int T = gx * gy;
     if (T == 0) return;
-    hipLaunchKernelGGL(k_render_fwd, dim3(2 * T), dim3(64), 0, st, W, H, gx, T, order, sched, ranges, point_list,
+    // grid for the worst case of the schedule: 2T blocks with halves only, 4T with quarters
+    hipLaunchKernelGGL(k_render_fwd, dim3((split4_fwd_bucket() > 0 ? 4 : 2) * T), dim3(64), 0, st, W, H, gx, T, order,
+                       sched, ranges, point_list,
                        rec, bg, out_color, out_depth, out_alpha, out_segment, n_contrib);
 }
 

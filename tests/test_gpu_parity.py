@@ -342,11 +342,13 @@ def _tile_queue(state, T):
     return sched, cnt, lst
 
 
-@pytest.mark.parametrize("split,rows", [((1, 1), 1), ((1, 0), 1), ((0, 1), 1), ((1, 1), 0), ((10, 256), 1)])
+@pytest.mark.parametrize("split,rows", [((1, 1), 1), ((1, 0), 1), ((0, 1), 1), ((1, 1), 0), ((10, 256), 1),
+                                        ((1, 0, 1), 1), ((7, 0, 9), 1), ((7, 0, 9), 0)])
 def test_split_tiles(gpu_available, oracle_mod, split, rows):
     """Long tiles get two waves.  Forward: tiles whose list length has bit length >= B
     (n >= 2^(B-1)) are rendered as top / bottom halves (pixel results bit-identical to the
-    one-wave tile).  Backward: it walks the forward's depth queue deepest first, and tiles
+    one-wave tile), and with a third entry Q, tiles with n >= 2^(Q-1) as four 8x8 quarter
+    waves (the last quarter to finish files the tile in the backward queue).  Backward: it walks the forward's depth queue deepest first, and tiles
     whose deepest contributor is at least D deep get a block of two waves, each reducing a
     partial record per instance, summed wave 0 + wave 1.  (B, D) = (1, 1) splits every
     non-empty tile; forced on a small scene, for the row-binning and the radix
@@ -360,20 +362,24 @@ def test_split_tiles(gpu_available, oracle_mod, split, rows):
     try:
         _C.set_option("rows_binning", rows)
         for mode in ("split", "none"):
-            bf, bd = split if mode == "split" else (0, 0)
+            bf, bd, bq = (tuple(split) + (0,))[:3] if mode == "split" else (0, 0, 0)
             _C.set_option("split_fwd_bucket", bf)
             _C.set_option("split_bwd_depth", bd)
+            _C.set_option("split4_fwd_bucket", bq)
             out[mode] = Hn.run_gsr(scene, cam, grads=grads)
     finally:
         _C.set_option("rows_binning", 1)
         _C.set_option("split_fwd_bucket", -1)  # the defaults
         _C.set_option("split_bwd_depth", -1)
+        _C.set_option("split4_fwd_bucket", -1)
     a, b = out["split"], out["none"]
     T = ((cam.width + 15) // 16) * ((cam.height + 15) // 16)
     rg = b["ranges"].reshape(-1, 2).astype(np.int64)
     lens = rg[:, 1] - rg[:, 0]
     sched, cnt, lst = _tile_queue(a, T)
     assert sched[0] == (0 if split[0] == 0 else int((lens >= (1 << (split[0] - 1))).sum())), "forward split count"
+    if len(split) > 2:
+        assert sched[1] == int((lens >= (1 << (split[2] - 1))).sum()) > 0, "forward quarter count"
     assert _tile_queue(b, T)[0][0] == 0
     # the queue: every tile with a contributor once, under ceil(depth / 16) (capped at 63)
     depth = a["n_contrib_tiles"].reshape(T, 256).max(1).astype(np.int64)
