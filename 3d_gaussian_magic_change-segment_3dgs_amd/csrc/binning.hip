@@ -570,10 +570,10 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
 // look-back (the inclusive prefix advanced 8 tiles per cross-XCD round trip: the last tiles
 // finished their look-back 9 us after the first), and identity passes (a constant top byte)
 // still cost a 7-us copy plus a launch gap.  Here:
-//   * tile index = blockIdx.x.  Tile t waits only on tiles < t; the dispatcher starts a
-//     kernel's workgroups in index order on each XCD, so the lowest unfinished tile has always
-//     started and its predecessors have finished: the waits terminate (and with <= 256 tiles
-//     of 1024 threads, every tile is resident at once anyway);
+//   * the tile index still comes from an atomic ticket in dispatch order (a tile waits only on
+//     tiles that have started, whatever order the hardware dispatches workgroups in and however
+//     many CUs a concurrent kernel -- RCCL's, in the data-parallel run -- holds), but the ticket's
+//     round trip now overlaps the load of the pass plan instead of preceding the key loads;
 //   * two-level look-back: a tile publishes its digit counts, sums those of the earlier tiles
 //     of its group of GRP_SIZE (independent loads, no chain), and the group's last tile
 //     publishes the group total; a tile adds the totals of the earlier groups.  About three
@@ -594,7 +594,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter_grp(GrpBufs B, siz
                                                                   int per_pass, int key_bits,
                                                                   const uint32_t* __restrict__ hist,
                                                                   uint64_t* status, const uint32_t* span,
-                                                                  int no_keys) {
+                                                                  int no_keys, uint32_t* counter) {
     constexpr int NT = 64 * WAVES, TILE = NT * ITEMS;
     ST_T(st0)
     __shared__ uint32_t s_key[TILE], s_val[TILE], s_val2[TILE];
@@ -602,11 +602,16 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter_grp(GrpBufs B, siz
     __shared__ uint32_t dbase[RADIX], gbase[RADIX];
     __shared__ uint32_t wsum[WAVES];
     const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-    const int t = (int)blockIdx.x, ntiles = (int)gridDim.x;
-    // the pass plan: real passes (span: the key bits that vary over the keys that matter)
+    // the key bits that vary over the keys that matter (k_radix_hist), loaded while the tile
+    // index is taken
+    const uint32_t vary = span[0] & span[1];
+    const int ntiles = (int)gridDim.x;
+    const int t = lb_tile_index(counter);
+    // the pass plan: real passes
     int nreal = 0, j = -1;
     for (int p = 0; p < passes; ++p) {
-        const bool real = !identity_pass(span, p * per_pass, min(per_pass, key_bits - p * per_pass));
+        const int sh = p * per_pass, nb = min(per_pass, key_bits - p * per_pass);
+        const bool real = ((vary >> sh) & ((1u << nb) - 1u)) != 0u;
         if (real) {
             if (p == pass) j = nreal;
             ++nreal;
@@ -1077,7 +1082,8 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
         for (int p = 0; p < passes; ++p)
             hipLaunchKernelGGL((k_radix_scatter_grp<GSR_LB_ITEMS, GSR_LB_WAVES>), dim3((unsigned)nt),
                                dim3(64 * GSR_LB_WAVES), 0, st, B, n, p, passes, per_pass, key_bits, W.hist,
-                               W.status + (size_t)p * sort_grp_status_words(nt), W.counter + SPAN_WORD, no_keys);
+                               W.status + (size_t)p * sort_grp_status_words(nt), W.counter + SPAN_WORD, no_keys,
+                               W.counter + p);
         return;
     }
     const uint32_t* kin = keys_in;
