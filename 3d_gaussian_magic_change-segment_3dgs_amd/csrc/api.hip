@@ -314,7 +314,7 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
     if (hslot) __atomic_store_n(hslot, TOTAL_PENDING, __ATOMIC_RELAXED);
     {
         StageScope sc(GSR_STAGE_PREPROCESS, st);
-        const bool lb = sort_uses_lookback(P);
+        const bool lb = sort_uses_lookback(P) || sort_grouped_size(P);  // look-back counters to clear
         launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
                           at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect),
                           packed ? at<uint32_t>(g, L.rect32) : nullptr, at<float>(g, L.shjac),

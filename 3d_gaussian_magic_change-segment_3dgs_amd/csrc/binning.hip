@@ -564,7 +564,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
 }
 
 // ------------------------------------------- grouped look-back passes ----
-// The depth sort's passes for grids of at most GRP_MAX_TILES tiles (1M keys at 4096 keys per
+// The depth sort's passes for grids of at most GRP_MAX_TILES tiles (4M keys at 4096 keys per
 // tile), measured per tile phase (tools/sort_trace.py, profiles/round3_sort_trace.txt): of a
 // 17.8-us pass, 2.1 us went to the atomic that hands out tile indices, 6.8 us to the decoupled
 // look-back (the inclusive prefix advanced 8 tiles per cross-XCD round trip: the last tiles
@@ -575,14 +575,44 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
 //     many CUs a concurrent kernel -- RCCL's, in the data-parallel run -- holds), but the ticket's
 //     round trip now overlaps the load of the pass plan instead of preceding the key loads;
 //   * two-level look-back: a tile publishes its digit counts, sums those of the earlier tiles
-//     of its group of GRP_SIZE (independent loads, no chain), and the group's last tile
+//     of its group of 16 or 32 tiles (independent loads, no chain), and the group's last tile
 //     publishes the group total; a tile adds the totals of the earlier groups.  About three
 //     round trips instead of one per 8 tiles;
 //   * the pass plan comes from the digit spans of every pass (k_radix_hist): passes that are
 //     the identity on the keys that matter return at once, and the real passes ping-pong so
 //     that the last real one writes the output arrays (buffers chosen on the device: no copy).
 // Results are identical to the other modes (same stable order on the keys that matter).
-constexpr int GRP_SIZE = 16, GRP_MAX_TILES = GRP_SIZE * GRP_SIZE;
+// Group size: 16 tiles up to 256 tiles (the 1M-key depth sort), 32 up to GRP_MAX_TILES = 1024
+// (4M keys; C3's 3M-key depth sort 0.202 -> 0.161 ms).  Beyond, the table passes stay faster:
+// grouped passes over C5's 1465 tiles (groups of 64) took 0.320 ms against 0.258.
+constexpr int GRP_MIN = 16, GRP_MAX_TILES = 1024;
+inline int grp_size(size_t nt) { return nt <= 256 ? 16 : 32; }
+// Sum of the published values of words [lo, hi) of one digit column (stride RADIX between
+// tiles / groups), LB_WIN loads in flight at a time.
+constexpr int LB_WIN = 16;
+__device__ __forceinline__ uint32_t lb_sum_window(uint64_t* col, int lo, int hi) {
+    uint32_t acc = 0;
+    for (int i = lo; i < hi;) {
+        uint64_t w[LB_WIN];
+#pragma unroll
+        for (int k = 0; k < LB_WIN; ++k) w[k] = i + k < hi ? lb_load(col + (size_t)(i + k) * RADIX) : LB_AGG;
+        bool stall = false;
+        uint32_t part = 0;
+#pragma unroll
+        for (int k = 0; k < LB_WIN; ++k) {
+            if (i + k >= hi) continue;
+            stall |= (w[k] >> 32) == 0;
+            part += (uint32_t)w[k];
+        }
+        if (stall) {
+            __builtin_amdgcn_s_sleep(1);
+            continue;
+        }
+        acc += part;
+        i += LB_WIN;
+    }
+    return acc;
+}
 struct GrpBufs {
     const uint32_t* kin;
     const uint32_t* v2in;
@@ -594,7 +624,7 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter_grp(GrpBufs B, siz
                                                                   int per_pass, int key_bits,
                                                                   const uint32_t* __restrict__ hist,
                                                                   uint64_t* status, const uint32_t* span,
-                                                                  int no_keys, uint32_t* counter) {
+                                                                  int no_keys, uint32_t* counter, int grp) {
     constexpr int NT = 64 * WAVES, TILE = NT * ITEMS;
     ST_T(st0)
     __shared__ uint32_t s_key[TILE], s_val[TILE], s_val2[TILE];
@@ -694,51 +724,15 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter_grp(GrpBufs B, siz
             wcnt[w][tid] = o;
             o += cw;
         }
-        const int g = t / GRP_SIZE, t0 = g * GRP_SIZE;
+        const int g = t / grp, t0 = g * grp;
         uint64_t* const aggs = status + tid;                                  // [tile][RADIX]
         uint64_t* const grps = status + (size_t)ntiles * RADIX + tid;         // [group][RADIX]
-        // earlier tiles of the group: all loads issued together, re-issued until published
-        uint32_t in_grp = 0;
-        for (int i = t0; i < t;) {
-            uint64_t w[GRP_SIZE];
-#pragma unroll
-            for (int k = 0; k < GRP_SIZE; ++k) w[k] = i + k < t ? lb_load(aggs + (size_t)(i + k) * RADIX) : LB_AGG;
-            bool stall = false;
-#pragma unroll
-            for (int k = 0; k < GRP_SIZE; ++k) {
-                if (stall || i + k >= t) continue;
-                if ((w[k] >> 32) == 0) {
-                    stall = true;
-                    continue;
-                }
-                in_grp += (uint32_t)w[k];
-            }
-            if (!stall) break;
-            // restart the group sum: some word was not published yet
-            in_grp = 0;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        if (t == t0 + GRP_SIZE - 1 && t + 1 < ntiles)  // the group's total, for the later groups
+        // earlier tiles of the group, then the totals of the earlier groups: windows of LB_WIN
+        // independent loads, a window re-read until all of it is published
+        const uint32_t in_grp = lb_sum_window(aggs, t0, t);
+        if (t == t0 + grp - 1 && t + 1 < ntiles)  // the group's total, for the later groups
             lb_store(grps + (size_t)g * RADIX, LB_AGG | (in_grp + tot));
-        uint32_t before = 0;
-        for (int i = 0; i < g;) {
-            uint64_t w[GRP_SIZE];
-#pragma unroll
-            for (int k = 0; k < GRP_SIZE; ++k) w[k] = i + k < g ? lb_load(grps + (size_t)(i + k) * RADIX) : LB_AGG;
-            bool stall = false;
-#pragma unroll
-            for (int k = 0; k < GRP_SIZE; ++k) {
-                if (stall || i + k >= g) continue;
-                if ((w[k] >> 32) == 0) {
-                    stall = true;
-                    continue;
-                }
-                before += (uint32_t)w[k];
-            }
-            if (!stall) break;
-            before = 0;
-            __builtin_amdgcn_s_sleep(1);
-        }
+        const uint32_t before = lb_sum_window(grps, 0, g);
         gbase[tid] = gstart + before + in_grp;
     }
     __syncthreads();
@@ -1036,7 +1030,12 @@ bool sort_uses_lookback(size_t n) { return n <= g_sort_lb_max; }
 #endif
 static bool g_sort_grouped = GSR_SORT_GROUPED;  // gsr_set_option("sort_grouped", 0 / 1)
 void set_sort_grouped(bool on) { g_sort_grouped = on; }
-size_t sort_grp_status_words(size_t nt) { return (nt + cdiv(nt, GRP_SIZE)) * RADIX; }
+size_t sort_grp_status_words(size_t nt) { return (nt + cdiv(nt, GRP_MIN)) * RADIX; }
+// grouped passes for sorts of up to GRP_MAX_TILES tiles (whatever sort_lookback_max, which at 0
+// forces the histogram-table passes for every sort)
+bool sort_grouped_size(size_t n) {
+    return g_sort_grouped && g_sort_lb_max > 0 && sort_tiles(n, sort_lb_items()) <= (size_t)GRP_MAX_TILES;
+}
 
 // A tile is 64 * WAVES * ITEMS elements; sort_tiles(n, WAVES * ITEMS / 4) counts them.
 template <int ITEMS, int WAVES, bool LB>
@@ -1065,16 +1064,16 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     const bool lb = sort_uses_lookback(n);
     // (an output key array that is the input one is supported only when the sorted keys are not
     // wanted: k_radix_scatter_grp then alternates the keys between the input and tmp arrays)
-    const bool grp = lb && g_sort_grouped && !n_dev && sort_tiles(n, sort_lb_items()) <= (size_t)GRP_MAX_TILES &&
+    const bool grp = sort_grouped_size(n) && !n_dev && !vals_in &&
                      (!final_out || (!final_out->ranges && final_out->zero16 == 0)) &&
                      (keys_out != keys_in || (final_out && final_out->no_keys));
-    if (lb) {
+    if (lb || grp) {
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);
         hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)cdiv(n, (size_t)HIST_THREADS * HIST_ITEMS)), dim3(HIST_THREADS), 0, st, keys_in,
                            n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel, n_dev);
     }
-    if (grp && !vals_in) {
+    if (grp) {
         // grouped look-back passes with the pass plan on the device (k_radix_scatter_grp)
         const size_t nt = sort_tiles(n, sort_lb_items());
         const GrpBufs B{keys_in, vals2_in, keys_tmp, vals_tmp, vals2_tmp, keys_out, vals_out, vals2_out};
@@ -1083,7 +1082,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
             hipLaunchKernelGGL((k_radix_scatter_grp<GSR_LB_ITEMS, GSR_LB_WAVES>), dim3((unsigned)nt),
                                dim3(64 * GSR_LB_WAVES), 0, st, B, n, p, passes, per_pass, key_bits, W.hist,
                                W.status + (size_t)p * sort_grp_status_words(nt), W.counter + SPAN_WORD, no_keys,
-                               W.counter + p);
+                               W.counter + p, grp_size(nt));
         return;
     }
     const uint32_t* kin = keys_in;

@@ -302,7 +302,8 @@ int depth_sort_passes();
 int sort_lb_items();
 bool sort_uses_lookback(size_t n);
 void set_sort_lookback_max(size_t n);
-void set_sort_grouped(bool on);  // grouped look-back passes for sorts of <= 256 tiles (default on)
+void set_sort_grouped(bool on);  // grouped look-back passes for sorts of <= 1024 tiles (default on)
+bool sort_grouped_size(size_t n);  // a key-only sort of n keys (e.g. the depth sort) takes the grouped passes
 // Both tile-order launchers also write order[T + SCHED_FWD_SPLIT]: the number of tiles in
 // length buckets >= the forward's split bucket (set_split_buckets; 0 = no split), and zero
 // the backward queue's counters (TileSched).  bwd_depth: the backward splits tiles whose
