@@ -269,8 +269,14 @@ GSR_API const char* gsr_last_error(void);
 GSR_API const char* gsr_version(void);
 /* ---- tuning / test hook (process-wide, not thread-safe against concurrent calls):
  * "sort_lookback_max": radix sorts of at most this many keys use the single-launch
- * look-back passes, larger ones the histogram-table passes (default 4194304).
- * Results are identical either way.  Returns 0, or non-zero for an unknown name. */
+ * look-back passes, larger ones the histogram-table passes (default 4194304; 0 forces the
+ * table passes for every sort).  "sort_grouped" (0/1, default 1): key-only sorts of at most
+ * 1024 tiles (4M keys, e.g. the depth sort) take the grouped look-back passes.
+ * "rows_binning" (0/1, default 1), "speculate" (0/1, default 1), "split_fwd_bucket" /
+ * "split4_fwd_bucket" (forward tiles with n >= 2^(B-1) instances on two / four waves; defaults
+ * 8 / 0 = off), "split_bwd_depth" (backward two-wave tiles; default 0 = off); a negative value
+ * restores a default.  Results are identical either way.  Returns 0, or non-zero for an unknown
+ * name. */
 GSR_API int gsr_set_option(const char* name, long long value);
 
 #ifdef __cplusplus
