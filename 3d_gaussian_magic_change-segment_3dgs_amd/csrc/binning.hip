@@ -583,13 +583,15 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter(
 //     that the last real one writes the output arrays (buffers chosen on the device: no copy).
 // Results are identical to the other modes (same stable order on the keys that matter).
 // Group size: 16 tiles up to 256 tiles (the 1M-key depth sort), 32 up to GRP_MAX_TILES = 1024
-// (4M keys; C3's 3M-key depth sort 0.202 -> 0.161 ms).  Beyond, the table passes stay faster:
-// grouped passes over C5's 1465 tiles (groups of 64) took 0.320 ms against 0.258.
+// (C3's 3M-key depth sort 0.202 -> 0.161 ms).  Sorts of more than 1024 tiles of 4096 keys use
+// tiles of 8192 keys (16 waves x 8), up to 8M keys; grouped passes over 1465 tiles of 4096 keys
+// (C5, groups of 64) took 0.320 ms against 0.258 for the table passes.
 constexpr int GRP_MIN = 16, GRP_MAX_TILES = 1024;
+constexpr int GRP_BIG_ITEMS = 8;  // keys per thread of the 8192-key tiles
 inline int grp_size(size_t nt) { return nt <= 256 ? 16 : 32; }
 // Sum of the published values of words [lo, hi) of one digit column (stride RADIX between
 // tiles / groups), LB_WIN loads in flight at a time.
-constexpr int LB_WIN = 16;
+template <int LB_WIN = 16>
 __device__ __forceinline__ uint32_t lb_sum_window(uint64_t* col, int lo, int hi) {
     uint32_t acc = 0;
     for (int i = lo; i < hi;) {
@@ -729,10 +731,12 @@ __global__ void __launch_bounds__(64 * WAVES) k_radix_scatter_grp(GrpBufs B, siz
         uint64_t* const grps = status + (size_t)ntiles * RADIX + tid;         // [group][RADIX]
         // earlier tiles of the group, then the totals of the earlier groups: windows of LB_WIN
         // independent loads, a window re-read until all of it is published
-        const uint32_t in_grp = lb_sum_window(aggs, t0, t);
+        // (8-deep windows with 8 keys per thread: the 16-deep ones pushed the kernel past 128 VGPRs)
+        constexpr int WIN = ITEMS > 4 ? 8 : 16;
+        const uint32_t in_grp = lb_sum_window<WIN>(aggs, t0, t);
         if (t == t0 + grp - 1 && t + 1 < ntiles)  // the group's total, for the later groups
             lb_store(grps + (size_t)g * RADIX, LB_AGG | (in_grp + tot));
-        const uint32_t before = lb_sum_window(grps, 0, g);
+        const uint32_t before = lb_sum_window<WIN>(grps, 0, g);
         gbase[tid] = gstart + before + in_grp;
     }
     __syncthreads();
@@ -1033,8 +1037,12 @@ void set_sort_grouped(bool on) { g_sort_grouped = on; }
 size_t sort_grp_status_words(size_t nt) { return (nt + cdiv(nt, GRP_MIN)) * RADIX; }
 // grouped passes for sorts of up to GRP_MAX_TILES tiles (whatever sort_lookback_max, which at 0
 // forces the histogram-table passes for every sort)
+// keys per tile of the grouped passes (in 256-key units): 4096 keys, or 8192 beyond 1024 tiles
+static int grp_items(size_t n) {
+    return sort_tiles(n, sort_lb_items()) <= (size_t)GRP_MAX_TILES ? sort_lb_items() : GRP_BIG_ITEMS * GSR_LB_WAVES / 4;
+}
 bool sort_grouped_size(size_t n) {
-    return g_sort_grouped && g_sort_lb_max > 0 && sort_tiles(n, sort_lb_items()) <= (size_t)GRP_MAX_TILES;
+    return g_sort_grouped && g_sort_lb_max > 0 && sort_tiles(n, grp_items(n)) <= (size_t)GRP_MAX_TILES;
 }
 
 // A tile is 64 * WAVES * ITEMS elements; sort_tiles(n, WAVES * ITEMS / 4) counts them.
@@ -1075,14 +1083,16 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     }
     if (grp) {
         // grouped look-back passes with the pass plan on the device (k_radix_scatter_grp)
-        const size_t nt = sort_tiles(n, sort_lb_items());
+        const bool big = grp_items(n) != sort_lb_items();
+        const size_t nt = sort_tiles(n, grp_items(n));
         const GrpBufs B{keys_in, vals2_in, keys_tmp, vals_tmp, vals2_tmp, keys_out, vals_out, vals2_out};
         const int no_keys = final_out && final_out->no_keys ? 1 : 0;
-        for (int p = 0; p < passes; ++p)
-            hipLaunchKernelGGL((k_radix_scatter_grp<GSR_LB_ITEMS, GSR_LB_WAVES>), dim3((unsigned)nt),
-                               dim3(64 * GSR_LB_WAVES), 0, st, B, n, p, passes, per_pass, key_bits, W.hist,
-                               W.status + (size_t)p * sort_grp_status_words(nt), W.counter + SPAN_WORD, no_keys,
-                               W.counter + p, grp_size(nt));
+        for (int p = 0; p < passes; ++p) {
+            auto kern = big ? k_radix_scatter_grp<GRP_BIG_ITEMS, GSR_LB_WAVES> : k_radix_scatter_grp<GSR_LB_ITEMS, GSR_LB_WAVES>;
+            hipLaunchKernelGGL(kern, dim3((unsigned)nt), dim3(64 * GSR_LB_WAVES), 0, st, B, n, p, passes, per_pass,
+                               key_bits, W.hist, W.status + (size_t)p * sort_grp_status_words(nt), W.counter + SPAN_WORD,
+                               no_keys, W.counter + p, grp_size(nt));
+        }
         return;
     }
     const uint32_t* kin = keys_in;
