@@ -1039,6 +1039,9 @@ size_t sort_grp_status_words(size_t nt) { return (nt + cdiv(nt, GRP_MIN)) * RADI
 // forces the histogram-table passes for every sort)
 // keys per tile of the grouped passes (in 256-key units): 4096 keys, or 8192 beyond 1024 tiles
 static int grp_items(size_t n) {
+#ifdef GSR_GRP_BIG_ALWAYS  // experiment: 8192-key tiles for every grouped sort
+    return GRP_BIG_ITEMS * GSR_LB_WAVES / 4;
+#endif
     return sort_tiles(n, sort_lb_items()) <= (size_t)GRP_MAX_TILES ? sort_lb_items() : GRP_BIG_ITEMS * GSR_LB_WAVES / 4;
 }
 bool sort_grouped_size(size_t n) {
