@@ -123,6 +123,9 @@ namespace {
 // the stream drains without the value appearing (or pinned memory is unavailable) the
 // total is copied the ordinary way.
 constexpr uint32_t TOTAL_PENDING = 0xFFFFFFFFu;
+// The word has ONE writer per call: the depth sort's histogram kernel when it runs (tally of
+// tiles_touched, geometry_impl sets t_tallied), otherwise the offsets scan / level-1 binning.
+thread_local bool t_tallied = false;
 struct HostSlot {
     uint32_t* host = nullptr;  // CPU view
     uint32_t* dev = nullptr;   // GPU view of the same pinned word
@@ -311,6 +314,8 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
     const bool packed = rect_packable(IL.gx, IL.gy);
     const HostSlot hs = host_total_slot();  // NULL views if pinned host memory is unavailable
     uint32_t* hslot = hs.host;
+    bool tallied = false;  // the depth sort's histogram kernel posts num_rendered
+    t_tallied = false;
     if (hslot) __atomic_store_n(hslot, TOTAL_PENDING, __ATOMIC_RELAXED);
     {
         StageScope sc(GSR_STAGE_PREPROCESS, st);
@@ -325,7 +330,9 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
     {
         // Depth order: 32-bit keys -> 4 passes (even: sorted keys land back in depth_keys).
         StageScope sc(GSR_STAGE_DEPTH_SORT, st);
-        const SortFinal nokeys{nullptr, nullptr, 0, true};  // only the order (+ rects) is used
+        // only the order (+ rects) is used; the histogram kernel also sums tiles_touched into the
+        // host-mapped num_rendered word (the binning kernels store the same value later)
+        const SortFinal nokeys{nullptr, nullptr, 0, true, at<uint32_t>(g, L.tiles_touched), hs.dev, &tallied};
         launch_radix_sort(at<uint32_t>(g, L.depth_keys), nullptr, at<uint32_t>(g, L.dkeys_alt),
                           at<uint32_t>(g, L.order_alt), at<uint32_t>(g, L.depth_keys), at<uint32_t>(g, L.order), P,
                           32, g + L.ws, /*ws_zeroed=*/true, st, packed ? at<uint32_t>(g, L.rect32) : nullptr,
@@ -333,6 +340,7 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
                           packed ? at<uint32_t>(g, L.rect32_sorted) : nullptr, &nokeys,
                           /*skip_sentinel=*/true);  // culled Gaussians (key ~0u) emit nothing
     }
+    t_tallied = tallied;
     GSR_STAGE("depth sort");
     // gsr_forward's speculative stage B with row binning computes the offsets and num_rendered
     // in its level-1 kernels (binning_rows.hip, fused mode): no scan here
@@ -341,11 +349,12 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
         StageScope sc(GSR_STAGE_SCAN, st);
         if (packed)  // tile counts from the depth-ordered packed rects: no gather
             launch_scan_inclusive_gather(at<uint32_t>(g, L.rect32_sorted), nullptr, at<uint32_t>(g, L.offsets), P,
-                                         g + L.ws_scan, /*ws_zeroed=*/true, st, hs.dev, /*rect_mode=*/true);
+                                         g + L.ws_scan, /*ws_zeroed=*/true, st, tallied ? nullptr : hs.dev,
+                                         /*rect_mode=*/true);
         else
             launch_scan_inclusive_gather(at<uint32_t>(g, L.tiles_touched), at<uint32_t>(g, L.order),
                                          at<uint32_t>(g, L.offsets), P, g + L.ws_scan, /*ws_zeroed=*/true, st,
-                                         hs.dev);
+                                         tallied ? nullptr : hs.dev);
     }
     GSR_STAGE("scan");
     if (!wait) return 0;  // gsr_forward's speculative stage B: waits after launching it
@@ -408,7 +417,7 @@ int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* b
                                     at<uint32_t>(b, BL.vals_alt), at<uint32_t>(b, BL.point_list),
                                     at<uint32_t>(b, BL.slot_vals), ranges, order, at<uint4>(b, BL.written),
                                     cdiv(cap, 16), cap, n_total, st, stage, /*fused=*/true,
-                                    n_dev ? host_total_slot().dev : nullptr);
+                                    n_dev && !t_tallied ? host_total_slot().dev : nullptr);
             };
             {
                 StageScope sc(GSR_STAGE_DUPLICATE, st);

@@ -287,25 +287,34 @@ __device__ __forceinline__ bool identity_pass(const uint32_t* span, int shift, i
 __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __restrict__ keys, size_t n,
                                                              int passes, int per_pass, int key_bits,
                                                              uint32_t* __restrict__ hist, uint32_t* span,
-                                                             int skip_sentinel, const uint32_t* n_dev) {
+                                                             int skip_sentinel, const uint32_t* n_dev,
+                                                             const uint32_t* __restrict__ tally,
+                                                             unsigned long long* tally_word, uint32_t* tally_host) {
     ST_T(st0)
     if (n_dev) n = min(n, (size_t)*n_dev);
     __shared__ uint32_t cnt[4][RADIX];
-    __shared__ uint32_t s_span[2];
+    __shared__ uint32_t s_span[3];
     if (threadIdx.x < RADIX)
 #pragma unroll
         for (int p = 0; p < 4; ++p) cnt[p][threadIdx.x] = 0;
-    if (threadIdx.x < 2) s_span[threadIdx.x] = 0;
+    if (threadIdx.x < 3) s_span[threadIdx.x] = 0;
     __syncthreads();
     uint32_t ork = 0, ornk = 0;
     // all loads issued before any use (a strided loop with one dependent load per
     // iteration is latency-bound)
     const size_t base = (size_t)blockIdx.x * HIST_THREADS * HIST_ITEMS + threadIdx.x;
-    uint32_t kk[HIST_ITEMS];
+    uint32_t kk[HIST_ITEMS], tsum = 0;
 #pragma unroll
     for (int i = 0; i < HIST_ITEMS; ++i) {
         const size_t idx = base + (size_t)i * HIST_THREADS;
         kk[i] = idx < n ? keys[idx] : 0u;
+    }
+    if (tally) {
+#pragma unroll
+        for (int i = 0; i < HIST_ITEMS; ++i) {
+            const size_t idx = base + (size_t)i * HIST_THREADS;
+            tsum += idx < n ? tally[idx] : 0u;
+        }
     }
 #ifdef GSR_SORT_TRACE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -340,11 +349,26 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
     }
     ork = wave_or(ork);
     ornk = wave_or(ornk);
+    if (tally) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) tsum += (uint32_t)__shfl_xor((int)tsum, o, 64);
+    }
     if ((threadIdx.x & 63) == 0) {
         if (ork) atomicOr(&s_span[0], ork);
         if (ornk) atomicOr(&s_span[1], ornk);
+        if (tsum) atomicAdd(&s_span[2], tsum);
     }
     __syncthreads();
+    if (tally && threadIdx.x == 0) {
+        // one 64-bit atomic carries both the sum and the count of blocks done, so the block
+        // that completes the count holds the whole sum (no fences); sums < 2^40
+        const unsigned long long mine = (1ull << 40) | s_span[2];
+        const unsigned long long old =
+            __hip_atomic_fetch_add(tally_word, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if ((old >> 40) + 1 == gridDim.x)
+            __hip_atomic_store(tally_host, (uint32_t)((old + mine) & ((1ull << 40) - 1)), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    }
     ST_T(st2)
     if (threadIdx.x < RADIX)
         for (int p = 0; p < passes; ++p)
@@ -1078,11 +1102,16 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     const bool grp = sort_grouped_size(n) && !n_dev && !vals_in &&
                      (!final_out || (!final_out->ranges && final_out->zero16 == 0)) &&
                      (keys_out != keys_in || (final_out && final_out->no_keys));
+    const bool tally = (lb || grp) && final_out && final_out->tally && final_out->tally_host && !n_dev;
+    if (final_out && final_out->tally_used) *final_out->tally_used = tally;
     if (lb || grp) {
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);
         hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)cdiv(n, (size_t)HIST_THREADS * HIST_ITEMS)), dim3(HIST_THREADS), 0, st, keys_in,
-                           n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel, n_dev);
+                           n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel, n_dev,
+                           tally ? final_out->tally : nullptr,
+                           reinterpret_cast<unsigned long long*>(W.counter + TALLY_WORD),
+                           final_out ? final_out->tally_host : nullptr);
     }
     if (grp) {
         // grouped look-back passes with the pass plan on the device (k_radix_scatter_grp)

@@ -85,8 +85,9 @@ inline ScanWs scan_ws(size_t n, void* p) {
     return {p, scan_ws_bytes(n), reinterpret_cast<uint32_t*>(c), reinterpret_cast<uint64_t*>(c + ALIGN)};
 }
 // Sort workspace header: words [0, passes) are the look-back tile counters, words
-// [SPAN_WORD, SPAN_WORD + 2) the OR of the keys and of their complements (k_radix_hist).
-constexpr int SPAN_WORD = 16;
+// [SPAN_WORD, SPAN_WORD + 2) the OR of the keys and of their complements (k_radix_hist);
+// [TALLY_WORD, TALLY_WORD + 2) one 64-bit word: blocks done << 40 | tally sum (k_radix_hist).
+constexpr int SPAN_WORD = 16, TALLY_WORD = 18;
 struct SortWs {
     void* base;
     size_t header;      // bytes of counter + pass histograms
@@ -291,6 +292,15 @@ struct SortFinal {
     uint4* zero;
     size_t zero16;
     bool no_keys;  // the sorted keys are not needed: the last pass writes none
+    // optional: the histogram kernel (look-back / grouped modes) also sums tally[0, n) and its
+    // last block stores the sum into tally_host (a host-mapped word): num_rendered from the
+    // depth sort's first kernel, before any binning kernel has run
+    // (set true when it does: the caller must then leave the word to it alone -- a later
+    // store of the same call's value could land after the host has re-armed the word for
+    // its next call)
+    const uint32_t* tally = nullptr;
+    uint32_t* tally_host = nullptr;
+    bool* tally_used = nullptr;
 };
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL = identity*/, uint32_t* keys_tmp,
                        uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,

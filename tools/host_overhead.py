@@ -1,0 +1,103 @@
+"""Host-side time of one fwd+bwd step through the drop-in GaussianRasterizer (GPU).
+
+Wraps the C entry points (gsr_forward, gsr_backward) to stamp perf_counter_ns around them
+and prints, per phase, the median host microseconds over the timed steps:
+  py_fwd_pre   step start -> gsr_forward entry (Python wrapper, argument checks, allocations)
+  c_fwd        inside gsr_forward (launches + the num_rendered wait)
+  fwd_to_bwd   gsr_forward exit -> gsr_backward entry (autograd, backward wrapper)
+  c_bwd        inside gsr_backward (launches)
+  py_bwd_post  gsr_backward exit -> step end
+The GPU idles before the backward render when py_fwd_pre + c_fwd + fwd_to_bwd exceeds the
+GPU time of the forward.  usage: python tools/host_overhead.py [config] [steps]"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import diff_gaussian_rasterization as dgr  # noqa: E402
+from diff_gaussian_rasterization import _C  # noqa: E402
+from gsr_tools.scene import config_scene_and_camera  # noqa: E402
+
+
+class _Stamped:
+    def __init__(self, fn, log, tag):
+        self.fn, self.log, self.tag = fn, log, tag
+        self.argtypes, self.restype = fn.argtypes, fn.restype
+
+    def __call__(self, *a):
+        self.log.append((self.tag + "_in", time.perf_counter_ns()))
+        r = self.fn(*a)
+        self.log.append((self.tag + "_out", time.perf_counter_ns()))
+        return r
+
+
+class _Lib:
+    def __init__(self, lib, log):
+        self._lib, self._log = lib, log
+        self.gsr_forward = _Stamped(lib.gsr_forward, log, "f")
+        self.gsr_backward = _Stamped(lib.gsr_backward, log, "b")
+
+    def __getattr__(self, k):
+        return getattr(self._lib, k)
+
+
+def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "mt"
+    steps = int(sys.argv[2]) if len(sys.argv) > 2 else 200
+    dev = torch.device("cuda", 0)
+    scene, cam = config_scene_and_camera(cfg)
+    leaf = lambda t: t.to(dev).contiguous().requires_grad_(True)
+    means3D, shs, opac = leaf(scene.means3D), leaf(scene.shs), leaf(scene.opacities)
+    scales, rots, segs = leaf(scene.scales), leaf(scene.rotations), leaf(scene.segments)
+    means2D = torch.zeros_like(means3D, requires_grad=True)
+    E = torch.empty(0, device=dev)
+    H, W = cam.height, cam.width
+    st = dgr.GaussianRasterizationSettings(
+        image_height=H, image_width=W, tanfovx=cam.tanfovx, tanfovy=cam.tanfovy, bg=torch.zeros(3, device=dev),
+        scale_modifier=1.0, viewmatrix=cam.world_view_transform.to(dev), projmatrix=cam.full_proj_transform.to(dev),
+        sh_degree=scene.sh_degree, campos=cam.camera_center.to(dev), prefiltered=False, debug=False)
+    gen = torch.Generator().manual_seed(1)
+    ups = [(torch.randn(c, H, W, generator=gen) * 1e-3).to(dev) for c in (3, 1, 1, 2)]
+    params = [means3D, shs, opac, scales, rots, segs, means2D]
+    log = []
+    _C._lib = _Lib(_C._lib, log)
+
+    def step():
+        log.append(("s", time.perf_counter_ns()))
+        color, radii, depth, alpha, segment = dgr.rasterize_gaussians(means3D, means2D, shs, E, segs, opac, scales,
+                                                                      rots, E, st)
+        g = torch.autograd.grad([color, depth, alpha, segment], params, ups)
+        log.append(("e", time.perf_counter_ns()))
+        return g
+
+    for _ in range(10):
+        step()
+    torch.cuda.synchronize()
+    log.clear()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        step()
+    torch.cuda.synchronize()
+    wall = (time.perf_counter() - t0) / steps * 1e6
+    ph = {k: [] for k in ("py_fwd_pre", "c_fwd", "fwd_to_bwd", "c_bwd", "py_bwd_post", "total")}
+    i = 0
+    while i < len(log):
+        seq = log[i:i + 6]
+        i += 6
+        if [t for t, _ in seq] != ["s", "f_in", "f_out", "b_in", "b_out", "e"]:
+            continue
+        t = [v for _, v in seq]
+        for k, a, b in (("py_fwd_pre", 0, 1), ("c_fwd", 1, 2), ("fwd_to_bwd", 2, 3), ("c_bwd", 3, 4),
+                        ("py_bwd_post", 4, 5), ("total", 0, 5)):
+            ph[k].append((t[b] - t[a]) / 1e3)
+    print(f"{cfg}: {len(ph['total'])} steps, wall {wall:.1f} us/step (GPU-synchronised loop)")
+    for k, v in ph.items():
+        print(f"  {k:12s} median {np.median(v):8.1f} us  p90 {np.percentile(v, 90):8.1f}")
+
+
+if __name__ == "__main__":
+    main()
