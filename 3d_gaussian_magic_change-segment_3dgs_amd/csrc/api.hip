@@ -3,6 +3,8 @@
 // the host bindings DGR/rasterize_points.cu:35-242.
 #include <stdio.h>
 #include <stdlib.h>
+
+#include <chrono>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -152,13 +154,22 @@ HostSlot host_total_slot() {
 }
 int wait_total(uint32_t* hslot, hipStream_t st, const uint32_t* dev_last, uint32_t* total) {
     if (hslot) {
+        // hipStreamQuery enqueues a marker behind the work in flight, whose system-scope
+        // release runs between the forward render and the backward launched after this wait
+        // (a 6.8 us idle gap per step when the stream was queried every 256 spins): the
+        // stream is queried only once the word is 5 ms late, then every millisecond.
+        using clk = std::chrono::steady_clock;
+        const clk::time_point t0 = clk::now();
+        long next_ms = 5;
         for (unsigned spin = 0;; ++spin) {
             const uint32_t v = __atomic_load_n(hslot, __ATOMIC_ACQUIRE);
             if (v != TOTAL_PENDING) {
                 *total = v;
                 return 0;
             }
-            if ((spin & 255u) == 255u) {
+            if ((spin & 255u) == 255u &&
+                std::chrono::duration_cast<std::chrono::milliseconds>(clk::now() - t0).count() >= next_ms) {
+                ++next_ms;
                 const hipError_t q = hipStreamQuery(st);
                 if (q == hipSuccess) {  // drained: read once more, then fall back
                     const uint32_t w = __atomic_load_n(hslot, __ATOMIC_ACQUIRE);
