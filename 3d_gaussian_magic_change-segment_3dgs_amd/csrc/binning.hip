@@ -270,8 +270,11 @@ __global__ void __launch_bounds__(SCAN_THREADS) k_scan(const uint32_t* __restric
 // Keys per thread of k_radix_hist: fewer, fuller blocks mean fewer global atomics at the
 // end (one per nonzero (pass, digit) per block).
 // 16 waves x 4 keys per thread per block (a 4-wave block with 16 keys per thread left
-// under one wave per SIMD at 1M keys: latency-bound, 16 us).
-constexpr int HIST_THREADS = 1024, HIST_ITEMS = 4;
+// under one wave per SIMD at 1M keys: latency-bound, 16 us; 2 or 8 keys measured no better
+// there).  Larger sorts keep the grid near 366 blocks (8 keys per thread up to 4M keys, 16
+// beyond): at 6M keys the 1465 blocks of 4096 keys issued ~1.5M global atomics (41 us).
+constexpr int HIST_THREADS = 1024;
+inline int hist_items(size_t n) { return n <= (2u << 20) ? 4 : n <= (4u << 20) ? 8 : 16; }
 __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x121, 0xF, 0xF, false);  // row_ror:1
     x |= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x122, 0xF, 0xF, false);  // row_ror:2
@@ -284,6 +287,7 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
 __device__ __forceinline__ bool identity_pass(const uint32_t* span, int shift, int bits) {
     return (((span[0] & span[1]) >> shift) & ((1u << bits) - 1u)) == 0u;
 }
+template <int HIST_ITEMS>
 __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __restrict__ keys, size_t n,
                                                              int passes, int per_pass, int key_bits,
                                                              uint32_t* __restrict__ hist, uint32_t* span,
@@ -1107,7 +1111,9 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     if (lb || grp) {
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);
-        hipLaunchKernelGGL(k_radix_hist, dim3((unsigned)cdiv(n, (size_t)HIST_THREADS * HIST_ITEMS)), dim3(HIST_THREADS), 0, st, keys_in,
+        const int hi = hist_items(n);
+        auto hist_kern = hi == 4 ? k_radix_hist<4> : hi == 8 ? k_radix_hist<8> : k_radix_hist<16>;
+        hipLaunchKernelGGL(hist_kern, dim3((unsigned)cdiv(n, (size_t)HIST_THREADS * hi)), dim3(HIST_THREADS), 0, st, keys_in,
                            n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel, n_dev,
                            tally ? final_out->tally : nullptr,
                            reinterpret_cast<unsigned long long*>(W.counter + TALLY_WORD),
