@@ -7,6 +7,7 @@
 #include <chrono>
 #include <mutex>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "gsr_internal.h"
@@ -72,6 +73,30 @@ struct StageScope {
 int fail(const std::string& msg) {
     g_last_error = msg;
     return 1;
+}
+
+// gsr.h gsr_backward contract guard: the colour source of each geom buffer's last forward.  The
+// forward stores the SH direction Jacobian in geom only when it evaluated SH itself, so a
+// backward given shs for a buffer whose forward took colors_precomp fails here instead of
+// reading that field uninitialised.  Host-side bookkeeping only (no device read, no sync);
+// a buffer the table does not hold (another process's, or evicted) is not checked.
+struct GeomSource {
+    int P;
+    bool sh;
+};
+std::mutex g_src_mu;
+std::unordered_map<const void*, GeomSource> g_src;
+void note_source(const void* geom, int P, bool sh) {
+    std::lock_guard<std::mutex> lk(g_src_mu);
+    if (g_src.size() >= 4096) g_src.clear();
+    g_src[geom] = GeomSource{P, sh};
+}
+int check_source(const void* geom, int P, bool sh) {
+    std::lock_guard<std::mutex> lk(g_src_mu);
+    const auto it = g_src.find(geom);
+    if (it == g_src.end() || it->second.P != P || !sh || it->second.sh) return 0;
+    return fail("[gsr] backward: shs given, but the forward of this geom buffer took colors_precomp (pass the "
+                "forward's colour source; include/gsr.h gsr_backward)");
 }
 
 // Launch errors are checked after every stage; in debug mode the stream is also
@@ -318,6 +343,7 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
     const int P = s->P;
     if (P == 0) return 0;
     if (!geom || !radii) return fail("[gsr] geom/radii buffers are NULL");
+    note_source(geom, P, in->shs != nullptr);
     hipStream_t st = (hipStream_t)stream;
     const bool dbg = s->debug != 0;
     const ImgLayout IL = img_layout(s->W, s->H);
@@ -335,7 +361,7 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
         launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
                           at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect),
                           packed ? at<uint32_t>(g, L.rect32) : nullptr, at<float>(g, L.shjac),
-                          g + L.ws, lb ? sort_lb_zero_bytes(P, depth_sort_passes(), sort_lb_items()) : 0,
+                          g + L.ws, lb ? sort_zero_bytes(P, depth_sort_passes()) : 0,
                           g + L.ws_scan, scan_ws_bytes(P), st);
     }
     GSR_STAGE("preprocess");
@@ -540,6 +566,7 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
     if (P == 0) return 0;
     if (!geom || !img || !radii || !alpha || !dL_dcolor || !dL_dsegment || !dL_ddepth || !dL_dalpha)
         return fail("[gsr] null buffer");
+    if (int rc = check_source(geom, P, in->shs != nullptr)) return rc;
     hipStream_t st = (hipStream_t)stream;
     const bool dbg = s->debug != 0;
     const size_t I = num_rendered > 0 ? (size_t)num_rendered : 0;
@@ -613,6 +640,8 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
         if (!V.geom || !V.img || !V.radii || !V.alpha || !V.dL_dcolor || !V.dL_dsegment || !V.dL_ddepth ||
             !V.dL_dalpha)
             return fail("[gsr] multiview: null buffer");
+        // each view's SH direction Jacobian comes from its forward (as in gsr_backward)
+        if (int rc = check_source(V.geom, P, in->shs != nullptr)) return rc;
         const size_t I = V.num_rendered > 0 ? (size_t)V.num_rendered : 0;
         const ImgLayout IL = img_layout(s->W, s->H);
         char* im = aligned_base(V.img);
@@ -648,6 +677,7 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
         w.contrib = contrib;
         w.written = written;
         w.rec = at<float4>(g, GL.rec);
+        w.shjac = at<float>(g, GL.shjac);
         w.view = s->viewmatrix;
         w.proj = s->projmatrix;
         w.campos = s->campos;
@@ -688,12 +718,14 @@ int gsr_sh_backward(int V, int P, int D, int M, const float* shs, const float* m
     if (V < 0 || P < 0 || D < 0 || D > 3 || M < 1 || M < (D + 1) * (D + 1))
         return fail("[gsr] sh backward: bad V / P / D / M");
     if (P == 0) return 0;
-    if (!shs || !means3D || (V > 0 && !sh_rows)) return fail("[gsr] sh backward: null argument");
+    if (!means3D || (V > 0 && !sh_rows)) return fail("[gsr] sh backward: null argument");
     if (V == 0) {
         if (dsh) (void)hipMemsetAsync(dsh, 0, (size_t)P * M * 3 * 4, (hipStream_t)stream);
         return 0;
     }
-    launch_sh_backward(P, D, M, shs, means3D, V, sh_rows, dsh, dmeans3D, (hipStream_t)stream);
+    (void)shs;
+    (void)dmeans3D;  // the views' direction terms are in dmeans3D already (the multi-view backward)
+    launch_sh_backward(P, D, M, means3D, V, sh_rows, dsh, (hipStream_t)stream);
     hipError_t e = hipGetLastError();
     if (e != hipSuccess) return fail(std::string("[gsr] sh backward: ") + hipGetErrorString(e));
     return 0;

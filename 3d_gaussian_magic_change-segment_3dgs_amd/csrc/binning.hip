@@ -1075,6 +1075,10 @@ static int grp_items(size_t n) {
 bool sort_grouped_size(size_t n) {
     return g_sort_grouped && g_sort_lb_max > 0 && sort_tiles(n, grp_items(n)) <= (size_t)GRP_MAX_TILES;
 }
+size_t sort_zero_bytes(size_t n, int passes) {
+    // the grouped passes' tiles (8192 keys beyond 1024 tiles of 4096) or the classic look-back's
+    return sort_lb_zero_bytes(n, passes, sort_grouped_size(n) ? grp_items(n) : sort_lb_items());
+}
 
 // A tile is 64 * WAVES * ITEMS elements; sort_tiles(n, WAVES * ITEMS / 4) counts them.
 template <int ITEMS, int WAVES, bool LB>
@@ -1110,7 +1114,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     if (final_out && final_out->tally_used) *final_out->tally_used = tally;
     if (lb || grp) {
         const size_t nt = sort_tiles(n, sort_lb_items());
-        if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_lb_zero_bytes(n, passes, sort_lb_items()), st);
+        if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_zero_bytes(n, passes), st);
         const int hi = hist_items(n);
         auto hist_kern = hi == 4 ? k_radix_hist<4> : hi == 8 ? k_radix_hist<8> : k_radix_hist<16>;
         hipLaunchKernelGGL(hist_kern, dim3((unsigned)cdiv(n, (size_t)HIST_THREADS * hi)), dim3(HIST_THREADS), 0, st, keys_in,

@@ -394,7 +394,10 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_count(int gx, int gy, int nch1,
     // ahead of the row map's loads would delay them)
     zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH + threadIdx.x, (size_t)gridDim.x * RB_CH);  // scan-2 words
     for (int t = blockIdx.x * RB_CH + threadIdx.x; t < gx * gy; t += gridDim.x * RB_CH) ranges[t] = make_uint2(0u, 0u);
-    if (blockIdx.x == 0 && threadIdx.x < TILE_BUCKET_WORDS) bucket_words[threadIdx.x] = 0u;
+    // (strided: GSR_RB_CH may be below TILE_BUCKET_WORDS; a word left set would push
+    // k_tile_order_counted's positions past the order array)
+    if (blockIdx.x == 0)
+        for (int t = threadIdx.x; t < TILE_BUCKET_WORDS; t += RB_CH) bucket_words[t] = 0u;
     BT_END(1, bt0, bt1, nch_)
     (void)nch_;
 }

@@ -258,6 +258,7 @@ struct MvView {
     const float* contrib;
     const uint8_t* written;
     const float4* rec;
+    const float* shjac;  // the view's SH direction Jacobian (its forward's GeomLayout::shjac)
     const float* view;
     const float* proj;
     const float* campos;
@@ -276,8 +277,9 @@ __host__ __device__ inline size_t sh_rows_floats(int P) { return sh_rows_campos(
 void launch_gaussian_backward_multiview(int P, int D, int M, float scale_modifier, const gsr_inputs& in,
                                         const MvArgs& a, const gsr_grads& g, float* shx, bool defer_sh,
                                         hipStream_t st);
-void launch_sh_backward(int P, int D, int M, const float* shs, const float* means3D, int V, const float* shx,
-                        float* dsh, float* dmeans3D, hipStream_t st);
+// dsh [P,M,3] = sum over V views' rows of basis(dir) x dRGB (reads means3D and the rows only)
+void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const float* shx, float* dsh,
+                        hipStream_t st);
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
                               const float* contrib, const uint8_t* written, const float4* rec,
@@ -314,6 +316,8 @@ bool sort_uses_lookback(size_t n);
 void set_sort_lookback_max(size_t n);
 void set_sort_grouped(bool on);  // grouped look-back passes for sorts of <= 1024 tiles (default on)
 bool sort_grouped_size(size_t n);  // a key-only sort of n keys (e.g. the depth sort) takes the grouped passes
+// bytes of the sort workspace a look-back / grouped sort of n keys needs zeroed (its tile size)
+size_t sort_zero_bytes(size_t n, int passes);
 // Both tile-order launchers also write order[T + SCHED_FWD_SPLIT]: the number of tiles in
 // length buckets >= the forward's split bucket (set_split_buckets; 0 = no split), and zero
 // the backward queue's counters (TileSched).  bwd_depth: the backward splits tiles whose

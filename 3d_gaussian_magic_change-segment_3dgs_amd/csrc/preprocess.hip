@@ -863,17 +863,18 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
 // ------------------------------------------------------- multi-view backward --
 // Parameter gradients of B views summed (gsr_backward_multiview).  Two kernels:
 //  k_gaussian_backward_mv: per Gaussian, loops over the views: record gather,
-//    computeCov2DCUDA + preprocessCUDA backward per view (the view's camera), sums
-//    dmean / dcov3D / dopacity / dsegments / dcolors over the views, writes each
-//    view's dmeans2D, derives dscales / drot ONCE from the summed dcov3D (linear),
-//    and leaves each view's clamped dRGB for the SH kernel;
-//  k_gaussian_backward_mv_sh: per Gaussian, its SH row staged once through LDS
-//    (64 rows per wave, coalesced), loops over the views for the SH direction
-//    gradient and the dsh basis products, stores dsh once and adds the direction
-//    term into dmeans3D.
+//    computeCov2DCUDA + preprocessCUDA backward per view (the view's camera) including
+//    the SH direction term from the direction Jacobian the view's forward stored (no SH
+//    row is read), sums dmean / dcov3D / dopacity / dsegments / dcolors over the views,
+//    writes each view's dmeans2D, derives dscales / drot ONCE from the summed dcov3D
+//    (linear), and leaves each view's clamped dRGB row for the dsh kernel;
+//  k_sh_dsh: per Gaussian, dsh = sum over the views of basis(dir) x dRGB from means3D
+//    and the rows (the SH exchange's rebuild after an all-gather of the rows, or the
+//    local batch), stored once through LDS as coalesced runs.
 // The shared inputs are read and the parameter gradients written once per batch.
-__global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, float scale_modifier, gsr_inputs in,
-                                                              MvArgs a, gsr_grads g, float* __restrict__ shx) {
+__global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int D, int M, float scale_modifier,
+                                                              gsr_inputs in, MvArgs a, gsr_grads g,
+                                                              float* __restrict__ shx) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const size_t chunk = sh_rows_floats(P);
     if (shx && idx < a.B) {  // each view's camera centre travels with its dRGB rows
@@ -924,11 +925,15 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, floa
         dop += q[6];
         dseg0 += q[3];
         dseg1 += q[4];
-        if (drgb_v) {
+        f3 dRGB = {0.f, 0.f, 0.f};  // the clamped colour gradient (backward.cu:72-74)
+        if (in.shs) {
             const uint8_t cbits = w.clamped[idx];
-            drgb_v[0] = (cbits & 1) ? 0.f : q[0];
-            drgb_v[1] = (cbits & 2) ? 0.f : q[1];
-            drgb_v[2] = (cbits & 4) ? 0.f : q[2];
+            dRGB = {(cbits & 1) ? 0.f : q[0], (cbits & 2) ? 0.f : q[1], (cbits & 4) ? 0.f : q[2]};
+        }
+        if (drgb_v) {
+            drgb_v[0] = dRGB.x;
+            drgb_v[1] = dRGB.y;
+            drgb_v[2] = dRGB.z;
         }
         const float* view = w.view;
         const float* proj = w.proj;
@@ -1005,6 +1010,22 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, floa
         dmz.y = (view[6] - view[7] * mul3) * ddepth;
         dmz.z = (view[10] - view[11] * mul3) * ddepth;
         dmean = dmean + dmz;
+        if (in.shs && D > 0) {
+            // the SH direction term of this view (backward.cu:109-111 + dnormvdv), from the
+            // Jacobian its forward stored: the same arithmetic as k_gaussian_backward
+            const float* J = jac_row(w.shjac, idx);
+            const f3 jx = {J[0], J[64], J[128]}, jy = {J[192], J[256], J[320]}, jz = {J[384], J[448], J[512]};
+            const f3 cam = {w.campos[0], w.campos[1], w.campos[2]};
+            const f3 v = m - cam;
+            const f3 dv = {dot3(jx, dRGB), dot3(jy, dRGB), dot3(jz, dRGB)};
+            const float sum2 = v.x * v.x + v.y * v.y + v.z * v.z;
+            const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
+            f3 dn;
+            dn.x = ((+sum2 - v.x * v.x) * dv.x - v.y * v.x * dv.y - v.z * v.x * dv.z) * invsum32;
+            dn.y = (-v.x * v.y * dv.x + (sum2 - v.y * v.y) * dv.y - v.z * v.y * dv.z) * invsum32;
+            dn.z = (-v.x * v.z * dv.x - v.y * v.z * dv.y + (sum2 - v.z * v.z) * dv.z) * invsum32;
+            dmean = dmean + dn;
+        }
         dmean_sum = dmean_sum + dmean;
     }
     if (g.dcolors) { g.dcolors[i3] = dcol.x; g.dcolors[i3 + 1] = dcol.y; g.dcolors[i3 + 2] = dcol.z; }
@@ -1013,7 +1034,6 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, floa
     if (g.dcov3D)
 #pragma unroll
         for (int i = 0; i < 6; ++i) g.dcov3D[6 * (size_t)idx + i] = dcv_sum[i];
-    // dmeans3D without the SH direction term (k_gaussian_backward_mv_sh adds it)
     if (g.dmeans3D) {
         g.dmeans3D[i3] = dmean_sum.x;
         g.dmeans3D[i3 + 1] = dmean_sum.y;
@@ -1067,122 +1087,41 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int M, floa
     }
 }
 
-// SH part of the multi-view backward.  STAGED: M == 16 with 16-B aligned rows, the
-// wave's 64 rows go through LDS both ways (coalesced 12 KB runs); otherwise rows are
-// read / written per thread.
+// dsh of the multi-view backward / the SH exchange: dsh[i] = sum over the views of
+// basis_v x dRGB_v (backward.cu:46-110, the views in order, so every rank of an exchange
+// computes the same bits; one view: the same products k_gaussian_backward stores).
+// STAGED: M == 16 with 16-B aligned rows, the wave's 64 output rows go through LDS
+// (coalesced 12-KB runs); otherwise a thread writes its own row.
 template <bool STAGED>
-__global__ void __launch_bounds__(256) k_gaussian_backward_mv_sh(int P, int D, int M, const float* __restrict__ shs,
-                                                                 const float* __restrict__ means3D, int V,
-                                                                 const float* __restrict__ shx,
-                                                                 float* __restrict__ dsh,
-                                                                 float* __restrict__ dmeans3D) {
+__global__ void __launch_bounds__(256) k_sh_dsh(int P, int D, int M, const float* __restrict__ means3D, int V,
+                                                const float* __restrict__ shx, float* __restrict__ dsh) {
     const size_t chunk = sh_rows_floats(P);
     __shared__ float rows[STAGED ? 4 : 1][STAGED ? 64 : 1][52];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wbase = blockIdx.x * blockDim.x + wave * 64;
     const int idx = wbase + lane;
     const bool live = idx < P;
-    if (STAGED) {
-        const float4* src = reinterpret_cast<const float4*>(shs + (size_t)wbase * 48);
-#pragma unroll
-        for (int r = 0; r < 12; ++r) {
-            const int f = lane + 64 * r;  // float4 index in the wave's 64-row run
-            const int row = f / 12, col = f - 12 * (f / 12);
-            if (wbase + row < P) *reinterpret_cast<float4*>(&rows[wave][row][4 * col]) = src[f];
-        }
-        __syncthreads();
-    } else if (!live) {
-        return;
-    }
-    ShRow Sreg;
-    if (!STAGED && live) Sreg.load(shs + (size_t)idx * M * 3, M, (D + 1) * (D + 1));
-    const float* Sl = rows[STAGED ? wave : 0][STAGED ? lane : 0];
-    auto S = [&](int i) -> f3 {
-        if (STAGED) return f3{Sl[3 * i], Sl[3 * i + 1], Sl[3 * i + 2]};
-        return Sreg(i);
-    };
+    if (!STAGED && !live) return;
     float acc[48];
 #pragma unroll
     for (int i = 0; i < 48; ++i) acc[i] = 0.f;
-    f3 dn_sum = {0.f, 0.f, 0.f};
     const f3 mean = live ? ld3(means3D + 3 * (size_t)idx) : f3{0.f, 0.f, 0.f};
     for (int v = 0; v < V; ++v) {  // views in order: every rank of an exchange sums identically
-        const float* rows = shx + (size_t)v * chunk;
-        const f3 dRGB = live ? ld3(rows + 3 * (size_t)idx) : f3{0.f, 0.f, 0.f};
+        const float* r = shx + (size_t)v * chunk;
+        const f3 dRGB = live ? ld3(r + 3 * (size_t)idx) : f3{0.f, 0.f, 0.f};
         if (dRGB.x == 0.f && dRGB.y == 0.f && dRGB.z == 0.f) continue;  // invisible in this view (or a zero gradient)
-        const f3 dir_orig = mean - ld3(rows + sh_rows_campos(P));
+        const f3 dir_orig = mean - ld3(r + sh_rows_campos(P));
         const f3 dir = dir_orig / sqrtf(dot3(dir_orig, dir_orig));
         float bas[16];
-#pragma unroll
-        for (int i = 0; i < 16; ++i) bas[i] = 0.f;
-        f3 dx = {0, 0, 0}, dy = {0, 0, 0}, dz = {0, 0, 0};
-        const float x = dir.x, y = dir.y, z = dir.z;
-        bas[0] = C_SH0;
-        if (D > 0) {
-            bas[1] = -C_SH1 * y; bas[2] = C_SH1 * z; bas[3] = -C_SH1 * x;
-            dx = -C_SH1 * S(3);
-            dy = -C_SH1 * S(1);
-            dz = C_SH1 * S(2);
-            if (D > 1) {
-                const float xx = x * x, yy = y * y, zz = z * z, xy = x * y, yz = y * z, xz = x * z;
-                bas[4] = C_SH2[0] * xy;
-                bas[5] = C_SH2[1] * yz;
-                bas[6] = C_SH2[2] * (2.f * zz - xx - yy);
-                bas[7] = C_SH2[3] * xz;
-                bas[8] = C_SH2[4] * (xx - yy);
-                dx = dx + (C_SH2[0] * y * S(4) + C_SH2[2] * 2.f * -x * S(6) + C_SH2[3] * z * S(7) +
-                           C_SH2[4] * 2.f * x * S(8));
-                dy = dy + (C_SH2[0] * x * S(4) + C_SH2[1] * z * S(5) + C_SH2[2] * 2.f * -y * S(6) +
-                           C_SH2[4] * 2.f * -y * S(8));
-                dz = dz + (C_SH2[1] * y * S(5) + C_SH2[2] * 2.f * 2.f * z * S(6) + C_SH2[3] * x * S(7));
-                if (D > 2) {
-                    bas[9] = C_SH3[0] * y * (3.f * xx - yy);
-                    bas[10] = C_SH3[1] * xy * z;
-                    bas[11] = C_SH3[2] * y * (4.f * zz - xx - yy);
-                    bas[12] = C_SH3[3] * z * (2.f * zz - 3.f * xx - 3.f * yy);
-                    bas[13] = C_SH3[4] * x * (4.f * zz - xx - yy);
-                    bas[14] = C_SH3[5] * z * (xx - yy);
-                    bas[15] = C_SH3[6] * x * (xx - 3.f * yy);
-                    dx = dx + (C_SH3[0] * S(9) * 3.f * 2.f * xy + C_SH3[1] * S(10) * yz +
-                               C_SH3[2] * S(11) * -2.f * xy + C_SH3[3] * S(12) * -3.f * 2.f * xz +
-                               C_SH3[4] * S(13) * (-3.f * xx + 4.f * zz - yy) + C_SH3[5] * S(14) * 2.f * xz +
-                               C_SH3[6] * S(15) * 3.f * (xx - yy));
-                    dy = dy + (C_SH3[0] * S(9) * 3.f * (xx - yy) + C_SH3[1] * S(10) * xz +
-                               C_SH3[2] * S(11) * (-3.f * yy + 4.f * zz - xx) + C_SH3[3] * S(12) * -3.f * 2.f * yz +
-                               C_SH3[4] * S(13) * -2.f * xy + C_SH3[5] * S(14) * -2.f * yz +
-                               C_SH3[6] * S(15) * -3.f * 2.f * xy);
-                    dz = dz + (C_SH3[1] * S(10) * xy + C_SH3[2] * S(11) * 4.f * 2.f * yz +
-                               C_SH3[3] * S(12) * 3.f * (2.f * zz - xx - yy) + C_SH3[4] * S(13) * 4.f * 2.f * xz +
-                               C_SH3[5] * S(14) * (xx - yy));
-                }
-            }
-        }
+        sh_basis(D, dir, bas);
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             acc[3 * i] += bas[i] * dRGB.x;
             acc[3 * i + 1] += bas[i] * dRGB.y;
             acc[3 * i + 2] += bas[i] * dRGB.z;
         }
-        const f3 dv = {dot3(dx, dRGB), dot3(dy, dRGB), dot3(dz, dRGB)};
-        // dnormvdv (auxiliary.h:107-117)
-        const f3 vv = dir_orig;
-        const float sum2 = vv.x * vv.x + vv.y * vv.y + vv.z * vv.z;
-        const float invsum32 = 1.0f / sqrtf(sum2 * sum2 * sum2);
-        f3 dn;
-        dn.x = ((+sum2 - vv.x * vv.x) * dv.x - vv.y * vv.x * dv.y - vv.z * vv.x * dv.z) * invsum32;
-        dn.y = (-vv.x * vv.y * dv.x + (sum2 - vv.y * vv.y) * dv.y - vv.z * vv.y * dv.z) * invsum32;
-        dn.z = (-vv.x * vv.z * dv.x - vv.y * vv.z * dv.y + (sum2 - vv.z * vv.z) * dv.z) * invsum32;
-        dn_sum = dn_sum + dn;
     }
-    if (live && dmeans3D) {
-        float* o = dmeans3D + 3 * (size_t)idx;
-        o[0] += dn_sum.x;
-        o[1] += dn_sum.y;
-        o[2] += dn_sum.z;
-    }
-    if (!dsh) return;  // uniform
     if (STAGED) {
-        __syncthreads();  // every lane has read its SH row
         float* row = rows[wave][lane];
 #pragma unroll
         for (int i = 0; i < 12; ++i)
@@ -1222,24 +1161,21 @@ void launch_gaussian_backward_multiview(int P, int D, int M, float scale_modifie
                                         const MvArgs& a, const gsr_grads& g, float* shx, bool defer_sh,
                                         hipStream_t st) {
     if (P == 0) return;
-    float* shx_used = (in.shs && (defer_sh || g.dsh || g.dmeans3D)) ? shx : nullptr;
+    float* shx_used = (in.shs && (defer_sh || g.dsh)) ? shx : nullptr;
     hipLaunchKernelGGL(k_gaussian_backward_mv, dim3(cdiv(P, 256)), dim3(256),
-                       0, st, P, M, scale_modifier, in, a, g, shx_used);
+                       0, st, P, D, M, scale_modifier, in, a, g, shx_used);
     if (!shx_used || defer_sh) return;
-    launch_sh_backward(P, D, M, in.shs, in.means3D, a.B, shx_used, g.dsh, g.dmeans3D, st);
+    launch_sh_backward(P, D, M, in.means3D, a.B, shx_used, g.dsh, st);
 }
 
-void launch_sh_backward(int P, int D, int M, const float* shs, const float* means3D, int V, const float* shx,
-                        float* dsh, float* dmeans3D, hipStream_t st) {
-    if (P == 0 || V == 0) return;
-    const bool staged = M == 16 && (reinterpret_cast<uintptr_t>(shs) & 15) == 0 &&
-                        (!dsh || (reinterpret_cast<uintptr_t>(dsh) & 15) == 0);
+void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const float* shx, float* dsh,
+                        hipStream_t st) {
+    if (P == 0 || V == 0 || !dsh) return;
+    const bool staged = M == 16 && (reinterpret_cast<uintptr_t>(dsh) & 15) == 0;
     if (staged)
-        hipLaunchKernelGGL(k_gaussian_backward_mv_sh<true>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, shs,
-                           means3D, V, shx, dsh, dmeans3D);
+        hipLaunchKernelGGL(k_sh_dsh<true>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, means3D, V, shx, dsh);
     else
-        hipLaunchKernelGGL(k_gaussian_backward_mv_sh<false>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, shs,
-                           means3D, V, shx, dsh, dmeans3D);
+        hipLaunchKernelGGL(k_sh_dsh<false>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, means3D, V, shx, dsh);
 }
 
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,

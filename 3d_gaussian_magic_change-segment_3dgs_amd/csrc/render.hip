@@ -27,10 +27,14 @@
 // pixel replays (behind every last contributor, or out of reach) write nothing.
 // The per-Gaussian backward kernel sums a Gaussian's written slots in slot
 // order: deterministic, atomic-free gradients.  Record (q = G * dL_dalpha per pixel,
-// d = (dx, dy) = mean2D - pixel):
-//   [sum dch*dL_dcolor.rgb, sum dch*dL_dseg0/1, sum dch*dL_ddepth,
-//    sum q, sum q dx, sum q dy, sum q dx^2, sum q dx dy, sum q dy^2]
-// from which k_gaussian_backward forms dopacity = sum q and the reference's
+// d = (dx, dy) = mean2D - pixel, conic (a, b, c)), 12 floats:
+//   [0..5]  sum dch*dL_dcolor.rgb, sum dch*dL_dseg0/1, sum dch*dL_ddepth
+//   [6]     sum q
+//   [7] [8] default: sum q (a dx + b dy), sum q (b dx + c dy)   (the reference's dG_ddelx /
+//           dG_ddely weighting, backward.cu:612-621, formed per lane before the reduction)
+//           GSR_MOMENT_MEAN builds: sum q dx, sum q dy
+//   [9..11] sum q dx^2, sum q dx dy, sum q dy^2
+// from which k_gaussian_backward (preprocess.hip) forms dopacity = sum q and the reference's
 // mean2D / conic gradients with the Gaussian's own conic and opacity.
 #include "gsr_internal.h"
 
@@ -72,11 +76,13 @@ __device__ __forceinline__ float gsr_expf(float x) {
     const float scale = __uint_as_float((__float_as_uint(kf) << 23) + 0x3f800000u);
     return p * scale;
 }
-// gsr_expf without the clamp, for lanes whose argument is known to lie in [-87, 88]: the
+// gsr_expf without the clamp, for lanes whose argument is known to lie in [-87, 0]: the
 // blend loops call it only under a lane mask of pixels with power >= the Gaussian's
 // opacity floor (>= -5.6) and use the result only under that mask (other lanes get a
 // meaningless, possibly non-finite value that every use masks out).  Same bits as
-// gsr_expf on that range.
+// gsr_expf on [-125 ln2, 0]: there p * 2^k is a normal number, so scaling by 2^k is exact
+// and equals adding k to p's exponent field -- one v_lshl_add_u32 instead of building 2^k
+// and multiplying.
 __device__ __forceinline__ float gsr_expf_nc(float x) {
     const float kf = __builtin_fmaf(x, 1.44269502f, 12582912.0f);
     const float k = kf - 12582912.0f;
@@ -89,8 +95,13 @@ __device__ __forceinline__ float gsr_expf_nc(float x) {
     p = __builtin_fmaf(p, r, 0.4999999403953552f);
     p = __builtin_fmaf(p, r, 1.0f);
     p = __builtin_fmaf(p, r, 1.0f);
+#ifdef GSR_EXP_MUL
     const float scale = __uint_as_float((__float_as_uint(kf) << 23) + 0x3f800000u);
     return p * scale;
+#else
+    // kf's low mantissa bits hold k (two's complement), so kf_bits << 23 == k << 23 (mod 2^32)
+    return __uint_as_float((__float_as_uint(kf) << 23) + __float_as_uint(p));
+#endif
 }
 #ifdef GSR_FAST_EXP
 #define GSR_EXP(x) __expf(x)
@@ -571,7 +582,7 @@ struct BwdShared {
     float part[2][64][12];  // split tiles: per-wave partial record of each batch instance
     float4 stage[2][64][3]; // unsplit tiles: per-wave records of the batch, stored at the next batch
     uint64_t tmask[2];      // split tiles: instances each wave produced a partial for
-    uint32_t top[2];        // split tiles: per-wave deepest contributor | use_bg << 31
+    uint32_t top[2];        // split tiles: per-wave deepest contributor
 };
 
 // LDS write -> read by other lanes of the SAME wave: a wave's LDS instructions execute in
@@ -618,7 +629,13 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
     // reference's sum_ch (c[ch] - accum_rec[ch]) * dL_dch is cdot - Dk.  Equal in exact
     // arithmetic; the fp32 rounding differs from the per-channel form at the 1e-7
     // level (tests/test_gpu_parity.py tolerances), and 24 registers per lane are freed.
-    float pfy[NS], T[NS], Tfin[NS], dp0[NS], dp1[NS], dp2[NS], ds0[NS], ds1[NS], dd[NS], da[NS], bgdot[NS];
+    // The background term of dL_dalpha, -T_final / (1 - alpha) * (bg . dL_dpix) per
+    // contributor (backward.cu:593-597), is the same recurrence's contribution of a virtual
+    // last contributor with colour bg (and 0 in the segment / depth / alpha channels) and
+    // alpha 1: Dk starts at bg . dL_dpix instead of 0, and (cdot - Dk) * T then carries
+    // -(bg . dL_dpix) T_final / (1 - alpha) at every contributor.  No bg-specialised loop, no
+    // T_final / bg . dL_dpix registers and no extra rcp per replayed pair.
+    float pfy[NS], T[NS], dp0[NS], dp1[NS], dp2[NS], ds0[NS], ds1[NS], dd[NS], da[NS];
     float Dk[NS];
     uint32_t lastc[NS];
     uint32_t maxlast = 0;
@@ -632,8 +649,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
         const int r = (lane >> 4) + 4 * (s0 + k), c = lane & 15;
         const int fidx = 64 * (2 * (r >> 3) + (c >> 3)) + 8 * (r & 7) + (c & 7);
         lastc[k] = inside ? n_contrib[(size_t)tile * TILE_PIX + fidx] : 0u;
-        Tfin[k] = inside ? 1.f - alphas[pix] : 0.f;
-        T[k] = Tfin[k];
+        T[k] = inside ? 1.f - alphas[pix] : 0.f;  // T_final (backward.cu:468)
         dp0[k] = inside ? dL_dpixels[pix] : 0.f;
         dp1[k] = inside ? dL_dpixels[HW + pix] : 0.f;
         dp2[k] = inside ? dL_dpixels[2 * HW + pix] : 0.f;
@@ -645,23 +661,16 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
         bgd += bg0 * dp0[k];
         bgd += bg1 * dp1[k];
         bgd += bg2 * dp2[k];
-        bgdot[k] = bgd;
-        Dk[k] = 0.f;
+        Dk[k] = bgd;
         maxlast = max(maxlast, lastc[k]);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) maxlast = max(maxlast, (uint32_t)__shfl_xor((int)maxlast, o, 64));
-    bool any_bg = false;
-#pragma unroll
-    for (int k = 0; k < NS; ++k) any_bg |= bgdot[k] != 0.f;
-    bool use_bg = wave_any(any_bg);
     int top0 = (int)__builtin_amdgcn_readfirstlane(maxlast);
     if constexpr (SPLIT) {  // both waves walk the same batches (their barriers pair up)
-        if (lane == 0) sh->top[wid] = (uint32_t)top0 | (use_bg ? 0x80000000u : 0u);
+        if (lane == 0) sh->top[wid] = (uint32_t)top0;
         __syncthreads();
-        const uint32_t t0 = sh->top[0], t1 = sh->top[1];
-        top0 = (int)max(t0 & 0x7FFFFFFFu, t1 & 0x7FFFFFFFu);
-        use_bg = ((t0 | t1) >> 31) != 0;
+        top0 = (int)max(sh->top[0], sh->top[1]);
     }
 
     const uint2 range = ranges[tile];
@@ -690,8 +699,6 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
         g_next = plist[max(top0 - 65 - lane, 0)];
         u_next = slist[max(top0 - 65 - lane, 0)];
     }
-    // The background term of dL_dalpha (backward.cu:597) is only live when bg . dL_dpix
-    // is non-zero somewhere in the tile: the loop is specialised on it.
     // Unsplit tiles park a batch's records in LDS (stage[j] = record of batch instance j) and
     // store them at the start of the next batch, ahead of its prefetch loads.  gfx950 counts
     // vector loads and stores in one in-order vmcnt: with the records stored inside the batch,
@@ -712,8 +719,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
             }
         }
     };
-    auto replay = [&](auto use_bg_c) {
-        constexpr bool UB = decltype(use_bg_c)::value;
+    auto replay = [&]() {
         for (int top = top0; top > 0; top -= 64) {
             const int cnt = min(64, top);
             STAT(5, 1);
@@ -786,7 +792,11 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                         continue;
                     }
 #endif
+#ifdef GSR_PFY_RECOMPUTE
+                    const float dy = gy_ - (pfy[0] + 4.f * k);  // the same exact pixel-centre float
+#else
                     const float dy = gy_ - pfy[k];
+#endif
                     dys[k] = dy;
                     power[k] = __builtin_fmaf(-0.5f, adxdx + cc * dy * dy, -(bdx * dy));  // == -0.5 S - B
                     near[k] = act[k] & __builtin_amdgcn_ballot_w64(power[k] >= pm);
@@ -837,7 +847,6 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                     cdot = __builtin_fmaf(dep, dd[k], cdot);
                     const float diff = cdot - Dk[k];
                     float dopa = diff * Tn;
-                    if (UB) dopa += (-Tfin[k] * __builtin_amdgcn_rcpf(one_m)) * bgdot[k];
 
                     acc[0] = __builtin_fmaf(dch_m, dp0[k], acc[0]);
                     acc[1] = __builtin_fmaf(dch_m, dp1[k], acc[1]);
@@ -919,10 +928,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
             }
         }
     };
-    if (use_bg)
-        replay(std::true_type{});
-    else
-        replay(std::false_type{});
+    replay();
     flush();
     STAT_FLUSH(16)
     WT_END(1, wslot, tile, n, top0, NS)
@@ -982,7 +988,10 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k
 }
 
 // No split (split_bwd_depth = 0): one wave per block and tile, deepest first.
-__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(4))) k_render_bwd1(
+#ifndef GSR_BWD1_WAVES
+#define GSR_BWD1_WAVES 4
+#endif
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD1_WAVES))) k_render_bwd1(
     int W, int H, int gx, int T, uint32_t* __restrict__ sched,
     const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ slot_vals,
     const float4* __restrict__ rec, const float* __restrict__ bg, const float* __restrict__ alphas,

@@ -308,10 +308,15 @@ def set_option(name, value):
 
 
 # Tuning experiments without a rebuild: GSR_OPTIONS="name=value,name=value" is applied at
-# import (e.g. GSR_OPTIONS="split_fwd_bucket=10,split_bwd_bucket=0").
-for _kv in filter(None, os.environ.get("GSR_OPTIONS", "").split(",")):
-    _k, _v = _kv.split("=")
-    set_option(_k.strip(), int(_v))
+# import (e.g. GSR_OPTIONS="split_fwd_bucket=10,split_bwd_depth=0").  A malformed or unknown
+# entry is reported and skipped: a typo in an environment variable must not break the import.
+for _kv in filter(None, (e.strip() for e in os.environ.get("GSR_OPTIONS", "").split(","))):
+    try:
+        _k, _v = _kv.split("=")
+        set_option(_k.strip(), int(_v))
+    except (ValueError, RuntimeError) as _e:
+        import warnings
+        warnings.warn(f"GSR_OPTIONS entry {_kv!r} ignored: {_e}")
 
 
 @functools.lru_cache(maxsize=64)
@@ -443,7 +448,9 @@ def sh_rows_floats(P):
 def sh_backward(sh_rows, V, means3D, sh, degree, dsh, dmeans3D):
     """gsr_sh_backward: from V views' SH exchange rows (sh_rows: fp32, V x
     sh_rows_floats(P), on the GPU), write dsh [P,M,3] = sum over the views of
-    basis x dRGB and add the SH direction term of every view to dmeans3D [P,3]."""
+    basis x dRGB.  The views' SH direction terms are already in dmeans3D (each rank
+    adds its own in the multi-view backward); `sh` gives M and `dmeans3D` is not
+    touched (both kept for the signature)."""
     P = int(means3D.size(0))
     M = int(sh.size(1))
     device = means3D.device

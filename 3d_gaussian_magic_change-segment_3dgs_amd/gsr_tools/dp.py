@@ -86,9 +86,83 @@ def exchange_bytes(world, views_per_rank, M=16):
             "sh_exchange": 2 * (n - 1) / n * 4 * 13 + (n - 1) * b * 12}
 
 
-def choose_exchange(world, views_per_rank, M=16):
-    c = exchange_bytes(world, views_per_rank, M)
-    return "sh" if c["sh_exchange"] < c["allreduce"] else "allreduce"
+# Time model of the exchange (us per step).  Link: xGMI, 153 GB/s per link and direction
+# (MI355X spec), of which RCCL is assumed to reach LINK_EFF; an 8-GPU node is fully
+# connected, so a rank's ring traffic can spread over its world - 1 peer links.  Both
+# numbers are assumptions until the driver's SCALE run measures them; they scale both
+# exchanges alike, so they matter only against the GPU-side costs below.
+LINK_GBPS = 153.0
+LINK_EFF = 0.7
+HBM_GBPS = 5000.0  # a streaming kernel's rate on MI355X (measured copy: 6.5 TB/s)
+
+
+def rebuild_bytes(P, views, M=16):
+    """HBM bytes of the SH exchange's dsh rebuild (gsr_sh_backward, k_sh_dsh): means3D,
+    each view's dRGB row, the dsh rows written."""
+    return (12 + 12 * int(views) + 12 * int(M)) * int(P)
+
+
+def exchange_cost(world, views_per_rank, P, M=16, compute_us=None, rebuild_us=None, link_gbps=None,
+                  hbm_gbps=HBM_GBPS):
+    """Modelled cost of both exchanges per step.  link_us: the ring traffic over the peer
+    links; gpu_us: HBM work the exchange adds on each GPU (RCCL's reductions ~3 passes over
+    the reduced bytes, the all-gathered rows, and for the SH exchange the dsh rebuild --
+    `rebuild_us` when it was measured, else modelled from rebuild_bytes).  The exchange of
+    step k overlaps step k+1's render, so a step costs max(compute + gpu, link) when the
+    compute time is known, gpu + link otherwise."""
+    n, b, P = int(world), int(views_per_rank), int(P)
+    if n <= 1:  # nothing crosses a link; the SH exchange still rebuilds dsh
+        rb = rebuild_us if rebuild_us is not None else rebuild_bytes(P, b, M) / (hbm_gbps * 1e3)
+        return {"allreduce": {"link_us": 0.0, "gpu_us": 0.0, "total_us": compute_us or 0.0},
+                "sh_exchange": {"link_us": 0.0, "gpu_us": round(rb, 2), "total_us": round((compute_us or 0.0) + rb, 2),
+                                "rebuild_us": round(rb, 2), "rebuild_measured": rebuild_us is not None}}
+    rate = (link_gbps or LINK_GBPS * LINK_EFF) * (n - 1) * 1e3  # bytes per us
+    by = exchange_bytes(n, b, M)
+    hbm = hbm_gbps * 1e3
+    red = 3 * (n - 1) / n
+    modelled_rebuild = rebuild_bytes(P, n * b, M) / hbm
+    gpu = {"allreduce": red * 4 * (13 + 3 * M) * P / hbm,
+           "sh_exchange": (red * 4 * 13 * P + 12 * n * b * P) / hbm +
+                          (rebuild_us if rebuild_us is not None else modelled_rebuild)}
+    out = {}
+    for k in ("allreduce", "sh_exchange"):
+        link_us = by[k] * P / rate
+        tot = max(compute_us + gpu[k], link_us) if compute_us else gpu[k] + link_us
+        out[k] = {"link_us": round(link_us, 2), "gpu_us": round(gpu[k], 2), "total_us": round(tot, 2)}
+    out["sh_exchange"]["rebuild_us"] = round(rebuild_us if rebuild_us is not None else modelled_rebuild, 2)
+    out["sh_exchange"]["rebuild_measured"] = rebuild_us is not None
+    return out
+
+
+def choose_exchange(world, views_per_rank, M=16, P=None, compute_us=None, rebuild_us=None):
+    """"sh" or "allreduce".  With P: the cheaper modelled step (exchange_cost, including the
+    measured or modelled dsh rebuild); without: the fewer link bytes."""
+    if P is None:
+        c = exchange_bytes(world, views_per_rank, M)
+        return "sh" if c["sh_exchange"] < c["allreduce"] else "allreduce"
+    c = exchange_cost(world, views_per_rank, P, M, compute_us=compute_us, rebuild_us=rebuild_us)
+    return "sh" if c["sh_exchange"]["total_us"] < c["allreduce"]["total_us"] else "allreduce"
+
+
+def measure_rebuild_us(P, M, views, device, degree=3, reps=5):
+    """Time gsr_sh_backward (the SH exchange's dsh rebuild) for `views` views' rows of P
+    Gaussians on this GPU: the median of `reps` launches, in us."""
+    from diff_gaussian_rasterization import _C
+    g = torch.Generator(device="cpu").manual_seed(0)
+    means3D = torch.randn(P, 3, generator=g).to(device)
+    rows = torch.randn(int(views) * _C.sh_rows_floats(P), generator=g).to(device) * 1e-3
+    dsh = torch.empty(P, M, 3, device=device)
+    sh = torch.empty(P, M, 3, device=device)
+    ts = []
+    for _ in range(reps + 1):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        _C.sh_backward(rows, int(views), means3D, sh, degree, dsh, None)
+        b.record()
+        b.synchronize()
+        ts.append(a.elapsed_time(b) * 1e3)
+    ts = sorted(ts[1:])
+    return ts[len(ts) // 2]
 
 
 def _all_gather_flat(out, inp, group, async_op):

@@ -141,8 +141,10 @@ def cpu_model():
 
 
 def cpu_baseline(scene, cam, grads, budget_s=20.0):
-    """The CPU oracle on whole views of the benchmark workload (fwd and bwd timed apart),
-    plus BASELINE config C1 (10k Gaussians, SH0, 256x256) for scale."""
+    """The CPU oracle on whole views of the benchmark workload (fwd and bwd timed apart), on
+    every CPU this process may run on (all host cores; `value`), and beside it
+    on the pool's CPU share for one GPU (OMP_NUM_THREADS as the box sets it), plus BASELINE
+    config C1 (10k Gaussians, SH0, 256x256) for scale."""
     from oracle import oracle as O
     from gsr_tools.scene import config_scene_and_camera
     O.build()
@@ -159,32 +161,44 @@ def cpu_baseline(scene, cam, grads, budget_s=20.0):
             tf += t1 - t0
         return tf, tb
 
-    one = sum(views(scene, cam, up, 1))  # warm-up view
-    reps = int(max(1, min(10, budget_s // max(one, 1e-3))))
-    tf, tb = views(scene, cam, up, reps)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
+    share = int(O.lib().oracle_num_threads())  # OMP_NUM_THREADS (the pool's share) or the runtime default
+
+    def timed(threads, budget):
+        O.lib().oracle_set_num_threads(threads)
+        one = sum(views(scene, cam, up, 1))  # warm-up view (thread pool, page faults)
+        reps = int(max(1, min(10, budget // max(one, 1e-3))))
+        tf, tb = views(scene, cam, up, reps)
+        return {"value": round(reps / (tf + tb), 4), "threads": threads, "fwd_ms_per_view": round(1e3 * tf / reps, 1),
+                "bwd_ms_per_view": round(1e3 * tb / reps, 1), "views": reps}
+
+    allc = timed(affinity or share, budget_s / 2)
+    pool = timed(share, budget_s / 2) if affinity and share != affinity else None
+    O.lib().oracle_set_num_threads(affinity or share)
     s1, c1 = config_scene_and_camera("c1")
     g1 = torch.Generator().manual_seed(1)
     up1 = [(torch.randn(c, c1.height, c1.width, generator=g1) * 1e-3).numpy() for c in (3, 2, 1, 1)]
     views(s1, c1, up1, 1)
     r1 = 20
     tf1, tb1 = views(s1, c1, up1, r1)
-    try:
-        affinity = len(os.sched_getaffinity(0))
-    except (AttributeError, OSError):
-        affinity = None
-    threads = int(O.lib().oracle_num_threads())
-    return {"value": round(reps / (tf + tb), 4), "unit": "views/s", "cores": threads,
-            "cores_note": (f"OpenMP threads used = {threads} (OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')}: "
-                           f"the pool's CPU share for one GPU); sched_getaffinity allows {affinity} of the "
-                           f"machine's os.cpu_count()={os.cpu_count()} logical CPUs, which other GPUs' jobs share"),
+    O.lib().oracle_set_num_threads(share)
+    return {"value": allc["value"], "unit": "views/s", "cores": allc["threads"],
+            "cores_note": (f"OpenMP threads = every CPU sched_getaffinity allows ({affinity} of the machine's "
+                           f"os.cpu_count()={os.cpu_count()} logical CPUs, shared with other GPUs' jobs); "
+                           f"'pool_share' = the same timed on OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')} "
+                           f"threads, the pool's CPU share for one GPU"),
             "affinity_cpus": affinity, "machine_cpus": os.cpu_count(),
             "kind": "port", "cpu_model": cpu_model(),
-            "fwd_ms_per_view": round(1e3 * tf / reps, 1), "bwd_ms_per_view": round(1e3 * tb / reps, 1),
+            "fwd_ms_per_view": allc["fwd_ms_per_view"], "bwd_ms_per_view": allc["bwd_ms_per_view"],
+            "pool_share": pool,
             "c1": {"value": round(r1 / (tf1 + tb1), 2), "unit": "views/s", "fwd_ms_per_view": round(1e3 * tf1 / r1, 2),
-                   "bwd_ms_per_view": round(1e3 * tb1 / r1, 2),
+                   "bwd_ms_per_view": round(1e3 * tb1 / r1, 2), "threads": affinity or share,
                    "sample": f"{r1} views of C1 (P={s1.P}, {c1.width}x{c1.height}, SH{s1.sh_degree})"},
-            "sample": f"{reps} whole fwd+bwd views of the benchmark workload (P={scene.P}, "
-                      f"{cam.width}x{cam.height}, SH{scene.sh_degree}) after 1 warm-up view; "
+            "sample": f"{allc['views']} whole fwd+bwd views of the benchmark workload (P={scene.P}, "
+                      f"{cam.width}x{cam.height}, SH{scene.sh_degree}) after 1 warm-up view, per thread count; "
                       f"oracle/gsr_oracle.cpp built -O3 -fopenmp"}
 
 
@@ -293,9 +307,15 @@ def main():
     pending = []  # the exchange in flight: (work handle, gradients kept alive)
 
     def exchange_kind(nv):
+        """The exchange for nv views per rank and its modelled cost (dp.exchange_cost), with the
+        SH exchange's dsh rebuild timed on this GPU at the step's view count (world * nv rows)."""
         if dist is None:
-            return None
-        return dp.choose_exchange(world, nv, shs.shape[1]) if args.exchange == "auto" else args.exchange
+            return None, None
+        M = shs.shape[1]
+        rb = dp.measure_rebuild_us(P, M, world * nv, device, degree=deg)
+        model = dp.exchange_cost(world, nv, P, M, rebuild_us=rb)
+        kind = dp.choose_exchange(world, nv, M, P=P, rebuild_us=rb) if args.exchange == "auto" else args.exchange
+        return kind, model
 
     def exchange(g, ex=None):
         # One exchange per step, on RCCL's stream (+ the SH completion on a side stream
@@ -316,7 +336,7 @@ def main():
             pending.pop()[0].wait()
 
     def make_step(nv):
-        kind = exchange_kind(nv)
+        kind, model = exchange_kind(nv)
 
         def step():
             ex = dp.ShExchange() if kind == "sh" else None
@@ -342,6 +362,7 @@ def main():
                                         params + means2D[:nv], up_list * nv)
             return g
         step.exchange = kind
+        step.exchange_model = model
         return step
 
     step = make_step(B)
@@ -469,11 +490,14 @@ def main():
         "step_ms": ({"mean": round(sum(step_ms) / len(step_ms), 4),
                      "median": round(sorted(step_ms)[len(step_ms) // 2], 4),
                      "p90": round(sorted(step_ms)[min(len(step_ms) - 1, int(0.9 * len(step_ms)))], 4),
-                     "max": round(max(step_ms), 4),
-                     "slowest": [(i, round(t, 3)) for t, i in sorted(((t, i) for i, t in enumerate(step_ms)),
-                                                                    reverse=True)[:5]],
-                     "source": f"hipEvents on the compute stream every {stride} steps, per-step means of "
-                               f"those windows (rank 0)"} if step_ms else None),
+                     "max_window": round(max(step_ms), 4),
+                     # (first step index of the window, its per-step mean): windows, not single steps
+                     "slowest_windows": [(i * stride, round(t, 3)) for t, i in
+                                         sorted(((t, i) for i, t in enumerate(step_ms)), reverse=True)[:5]],
+                     "window_steps": stride,
+                     "source": f"hipEvents on the compute stream every {stride} steps; every statistic is over "
+                               f"the per-step means of those {stride}-step windows, so a single slow step is "
+                               f"diluted by its window (rank 0)"} if step_ms else None),
         "vs_baseline": None, "dtype": "f32", "data": "synthetic (SURVEY.md s8d generator, seed 0; upstream grads "
                                                     "N(0,1)*1e-3 seed 1)",
         "config": {"workload": f"{args.config}: P={P} Gaussians, SH{deg}, {W}x{H}, fwd+bwd per view; {B} view(s) per "
@@ -488,6 +512,10 @@ def main():
                    "rccl_version": dinfo["rccl_version"]},
         "roofline": roof,
         "stages": stages,
+        "exchange": ({"chosen": step.exchange, "mode": args.exchange, "model_us": step.exchange_model,
+                      "model": "gsr_tools/dp.py exchange_cost: ring bytes over world-1 xGMI links at "
+                               f"{dp.LINK_GBPS:g} GB/s x {dp.LINK_EFF:g} (assumed), HBM work at {dp.HBM_GBPS:g} GB/s, "
+                               "the SH rebuild timed on this GPU"} if dist is not None else None),
     }
     out["batched"] = None
     if BB > 1 and BB != B:
@@ -503,7 +531,7 @@ def main():
         out["batched"] = {"views_per_step_per_gpu": BB, "global_batch": world * BB, "steps": k,
                           "value": round(world * BB * k / el_b, 2), "unit": "views/s",
                           "ms_per_step": round(1e3 * el_b / k, 4),
-                          "exchange": bstep.exchange,
+                          "exchange": bstep.exchange, "exchange_model_us": bstep.exchange_model,
                           "note": "per-view forward + one gsr_backward_multiview over the batch + one exchange"}
     out["train_step"] = None
     if rank == 0 and world == 1 and not args.no_train:

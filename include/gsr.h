@@ -157,8 +157,10 @@ GSR_API int gsr_forward(const gsr_settings* s, const gsr_inputs* in, void* geom,
  * Contract: `in` must name the same colour source as the forward of this geom buffer
  * (shs, or colors_precomp) with the same tensors.  The forward stores the SH direction
  * Jacobian in geom only when it evaluated SH itself; a backward given shs after a
- * forward with colors_precomp would read that field uninitialised.  (The reference
- * recomputes it from shs; the Python layer always passes the forward's inputs.) */
+ * forward with colors_precomp would read that field uninitialised: libgsr records each
+ * geom buffer's colour source at its forward and fails such a call (nonzero return,
+ * gsr_last_error) instead.  (The reference recomputes it from shs; the Python layer always
+ * passes the forward's inputs.) */
 GSR_API int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, void* geom,
                  void* binning, void* img, int num_rendered, const float* alpha,
                  const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
@@ -198,21 +200,24 @@ GSR_API int gsr_backward_multiview(int B, const gsr_view_state* views, const gsr
  * colour gradient) and the camera centre.  A data-parallel trainer therefore
  * exchanges each view's dRGB rows (all-gather, 12 B per Gaussian and view) instead
  * of all-reducing dsh (192 B per Gaussian), and every rank rebuilds the summed dsh
- * and the SH direction term of dmeans3D locally with gsr_sh_backward.
+ * locally with gsr_sh_backward.  The SH direction term of dmeans3D (dRGB . d(rgb)/d(dir),
+ * backward.cu:54-111) is added by each rank for its own views inside the multi-view
+ * backward, from the direction Jacobian each view's forward stored (36 B per Gaussian),
+ * so dmeans3D is complete before it is all-reduced and the rebuild reads no SH row.
  *
  * gsr_sh_rows_floats(P): floats of one view's rows: dRGB [P,3], then the view's
  * camera centre (x, y, z, 0) at float offset roundup(3P, 64).
  *
  * gsr_backward_multiview_deferred_sh: gsr_backward_multiview (shs required) that
  * writes the B views' rows to sh_rows [B][gsr_sh_rows_floats(P)] (16-B aligned)
- * and leaves grads->dsh unwritten and grads->dmeans3D WITHOUT the SH direction
- * term; all other gradients are complete (summed over the B views).
+ * and leaves grads->dsh unwritten; all other gradients, dmeans3D included, are
+ * complete (summed over the B views).
  *
  * gsr_sh_backward: for V views' rows (in order; every rank sums in the same order,
  * so all ranks get identical bits), writes dsh [P,M,3] = sum_v basis_v x dRGB_v
- * (coefficients >= (D+1)^2 written as 0) and ADDS the SH direction term of every
- * view to dmeans3D [P,3] (either may be NULL).  Run after the non-SH gradients are
- * all-reduced, the result equals the all-reduce of the complete gradients. */
+ * (coefficients >= (D+1)^2 written as 0).  Reads means3D and the rows only: shs and
+ * dmeans3D are accepted for ABI compatibility and not used (shs may be NULL).  Run on
+ * the all-gathered rows, the result equals the all-reduce of the complete dsh. */
 GSR_API size_t gsr_sh_rows_floats(int P);
 GSR_API int gsr_backward_multiview_deferred_sh(int B, const gsr_view_state* views, const gsr_inputs* in,
                                                float* sh_rows, const gsr_grads* grads, void* stream);

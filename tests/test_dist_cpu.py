@@ -135,20 +135,18 @@ def _sh_terms_f64(means3D, shs, deg, campos, drgb):
 
 
 def _sh_backward_f64(rows_all, V, means3D, sh, degree, dsh, dmeans3D):
-    """Stand-in for _C.sh_backward on CPU tensors (reads the same row layout)."""
+    """Stand-in for _C.sh_backward on CPU tensors (reads the same row layout): dsh only --
+    the direction term of dmeans3D is each rank's own, added before the exchange."""
     from diff_gaussian_rasterization._C import sh_rows_floats
     P = means3D.shape[0]
     ch = sh_rows_floats(P)
     cpos = ch - 64
     acc_sh = torch.zeros(sh.shape, dtype=torch.float64)
-    acc_dn = torch.zeros(P, 3, dtype=torch.float64)
     for v in range(V):
         r = rows_all[v * ch:(v + 1) * ch]
-        a, b = _sh_terms_f64(means3D, sh, degree, r[cpos:cpos + 3], r[:3 * P].view(P, 3))
+        a, _ = _sh_terms_f64(means3D, sh, degree, r[cpos:cpos + 3], r[:3 * P].view(P, 3))
         acc_sh += a
-        acc_dn += b
     dsh.copy_(acc_sh.float())
-    dmeans3D.add_(acc_dn.float())
 
 
 def _sh_scene():
@@ -166,13 +164,11 @@ def _sh_worker(rank, world, port, out_q):
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
     scene, cams = _sh_scene()
     g, M = _per_view_grads(rank)
-    # deferred form of this view's gradients: dRGB rows + dmeans3D without the SH
-    # direction term, dsh left as garbage (the exchange must overwrite all of it)
+    # deferred form of this view's gradients: dRGB rows + the complete dmeans3D (its SH
+    # direction term included), dsh left as garbage (the exchange must overwrite all of it)
     drgb = torch.from_numpy(g["dsh"][:, 0, :]).float() / C0
     campos = cams[rank].camera_center.float()
-    _, dn = _sh_terms_f64(scene.means3D, scene.shs, 3, campos, drgb)
     g = dict(g)
-    g["dmeans3D"] = (torch.from_numpy(g["dmeans3D"]).double() - dn).float().numpy()
     g["dsh"] = np.full_like(g["dsh"], np.nan)
     arena = dp.pack_arena(g, P_TEST, M)
     lay = dp.arena_layout(P_TEST, M)
@@ -224,3 +220,23 @@ def test_exchange_choice():
     assert dp.choose_exchange(8, 8) == "allreduce"
     c = dp.exchange_bytes(2, 1)
     assert c["allreduce"] / c["sh_exchange"] > 3.5
+
+
+def test_exchange_time_model():
+    """dp.exchange_cost / choose_exchange with P: the link time and the GPU-side work of both
+    exchanges (the choice must include the SH rebuild's measured cost)."""
+    from gsr_tools import dp
+    P = 1_000_000
+    c = dp.exchange_cost(8, 1, P, rebuild_us=55.0)
+    assert c["sh_exchange"]["total_us"] < c["allreduce"]["total_us"]
+    assert c["sh_exchange"]["rebuild_measured"] and c["sh_exchange"]["rebuild_us"] == 55.0
+    assert dp.choose_exchange(2, 1, P=P, rebuild_us=40.0) == "sh"
+    assert dp.choose_exchange(8, 8, P=P) == "allreduce"
+    # a rebuild slower than the link time it saves flips the choice
+    assert dp.choose_exchange(8, 1, P=P, rebuild_us=5000.0) == "allreduce"
+    # with the compute time known, an exchange hidden behind the render costs only its GPU work
+    h = dp.exchange_cost(8, 1, P, compute_us=930.0, rebuild_us=55.0)
+    assert h["allreduce"]["total_us"] == round(930.0 + h["allreduce"]["gpu_us"], 2)
+    assert dp.exchange_cost(1, 1, P)["allreduce"]["link_us"] == 0.0
+    m = dp.rebuild_bytes(P, 8)
+    assert m == (12 + 96 + 192) * P

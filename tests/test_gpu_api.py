@@ -223,3 +223,36 @@ def test_absent_input_gradients_are_not_aliased_views(gpu_available):
     for i in (0, 1, 3, 4, 5, 8):
         assert grads[i] is not None and 0 not in grads[i].stride(), f"input {i}"
         grads[i].add_(0.0)  # writable in place
+
+
+def test_backward_rejects_sh_after_colors_precomp_forward(gpu_available):
+    """the C ABI's colour-source contract (include/gsr.h gsr_backward) is guarded.
+    A backward given shs for a geom buffer whose forward took colors_precomp would read the SH
+    direction Jacobian the forward never wrote; libgsr fails that call (RuntimeError through the
+    binding) instead of returning garbage gradients with rc 0.  The matching call succeeds."""
+    from diff_gaussian_rasterization import _C
+    scene = synthetic_scene(3000, sh_degree=3, seed=72)
+    cam = orbit_camera(1, 96, 64, 80.0)
+    st = Hn.settings_for(cam, 3, "cuda")
+    dev = "cuda"
+    means3D, opac, segs = scene.means3D.to(dev), scene.opacities.to(dev), scene.segments.to(dev)
+    scales, rots, shs = scene.scales.to(dev), scene.rotations.to(dev), scene.shs.to(dev)
+    cols = torch.rand(scene.P, 3, device=dev)
+    E = torch.Tensor([])
+    fwd = _C.rasterize_gaussians(st.bg, means3D, cols, segs, opac, scales, rots, st.scale_modifier, E,
+                                 st.viewmatrix, st.projmatrix, st.tanfovx, st.tanfovy, st.image_height,
+                                 st.image_width, E, st.sh_degree, st.campos, st.prefiltered, st.debug)
+    R, color, depth, segment, alpha, radii, geom, binning, img = fwd
+    assert R > 0
+    ups = (torch.randn_like(color), torch.randn_like(segment), torch.randn_like(depth), torch.randn_like(alpha))
+
+    def backward(colors, sh):
+        return _C.rasterize_gaussians_backward(st.bg, means3D, radii, colors, segs, scales, rots, st.scale_modifier,
+                                               E, st.viewmatrix, st.projmatrix, st.tanfovx, st.tanfovy, *ups, sh,
+                                               st.sh_degree, st.campos, geom, R, binning, img, alpha, st.debug)
+
+    with pytest.raises(RuntimeError, match="colors_precomp"):
+        backward(E, shs)
+    g = backward(cols, E)
+    torch.cuda.synchronize()
+    assert torch.isfinite(g[3]).all() and float(g[1].abs().sum()) > 0

@@ -1,7 +1,7 @@
 #!/bin/bash
 # opt_sweep.sh "OPTS1" "OPTS2" ...: one short bench per GSR_OPTIONS string (stage table), twice
 # over in alternating order so drift between runs shows.  "" = defaults.
-# e.g. tools/opt_sweep.sh "" "prio_fwd_len=2048" "prio_bwd_depth=512"
+# e.g. tools/opt_sweep.sh "" "split_fwd_bucket=10" "split_bwd_depth=512"
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 STEPS=${STEPS:-60}
