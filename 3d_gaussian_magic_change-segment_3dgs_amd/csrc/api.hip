@@ -263,10 +263,16 @@ const char* gsr_version(void) { return "gsr 0.1 (gfx950)"; }
 
 static bool g_speculate = getenv("GSR_SPECULATE") == nullptr || getenv("GSR_SPECULATE")[0] != '0';
 static bool g_rows_binning = getenv("GSR_ROWS_BINNING") == nullptr || getenv("GSR_ROWS_BINNING")[0] != '0';
+// the multi-view backward's second stream (backward_multiview_impl)
+static bool g_mv_streams = getenv("GSR_MV_STREAMS") == nullptr || getenv("GSR_MV_STREAMS")[0] != '0';
 int gsr_set_option(const char* name, long long value) {
     if (!name) return fail("[gsr] option name is NULL");
     if (std::string(name) == "speculate") {  // gsr_forward's speculative stage B (default on)
         g_speculate = value != 0;
+        return 0;
+    }
+    if (std::string(name) == "mv_streams") {  // multi-view backward on two streams (default on)
+        g_mv_streams = value != 0;
         return 0;
     }
     if (std::string(name) == "rows_binning") {  // binning_rows.hip for grids <= 255 x 255 tiles (default on)
@@ -554,10 +560,38 @@ int gsr_forward(const gsr_settings* s, const gsr_inputs* in, void* geom, int* ra
                               out_segment, stream);
 }
 
+namespace {
+int backward_impl(const gsr_settings* s, const gsr_inputs* in, const int* radii, void* geom, void* binning,
+                  void* img, int num_rendered, const float* alpha, const float* dL_dcolor, const float* dL_dsegment,
+                  const float* dL_ddepth, const float* dL_dalpha, void* scratch, const gsr_grads* grads,
+                  float* sh_rows, void* stream);
+}  // namespace
+
 int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, void* geom, void* binning,
                  void* img, int num_rendered, const float* alpha, const float* dL_dcolor, const float* dL_dsegment,
                  const float* dL_ddepth, const float* dL_dalpha, void* scratch, const gsr_grads* grads,
                  void* stream) {
+    return backward_impl(s, in, radii, geom, binning, img, num_rendered, alpha, dL_dcolor, dL_dsegment, dL_ddepth,
+                         dL_dalpha, scratch, grads, nullptr, stream);
+}
+
+int gsr_backward_deferred_sh(const gsr_settings* s, const gsr_inputs* in, const int* radii, void* geom,
+                             void* binning, void* img, int num_rendered, const float* alpha, const float* dL_dcolor,
+                             const float* dL_dsegment, const float* dL_ddepth, const float* dL_dalpha,
+                             void* scratch, const gsr_grads* grads, float* sh_rows, void* stream) {
+    if (!sh_rows || !in || !in->shs) {
+        g_last_error = "[gsr] deferred SH backward: sh_rows and shs are required";
+        return 1;
+    }
+    return backward_impl(s, in, radii, geom, binning, img, num_rendered, alpha, dL_dcolor, dL_dsegment, dL_ddepth,
+                         dL_dalpha, scratch, grads, sh_rows, stream);
+}
+
+namespace {
+int backward_impl(const gsr_settings* s, const gsr_inputs* in, const int* radii, void* geom, void* binning,
+                  void* img, int num_rendered, const float* alpha, const float* dL_dcolor, const float* dL_dsegment,
+                  const float* dL_ddepth, const float* dL_dalpha, void* scratch, const gsr_grads* grads,
+                  float* sh_rows, void* stream) {
     using namespace gsr;
     g_last_error.clear();
     if (int rc = validate(s, in, false)) return rc;
@@ -594,13 +628,16 @@ int gsr_backward(const gsr_settings* s, const gsr_inputs* in, const int* radii, 
     }
     {
         StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);
+        gsr_grads gr = *grads;
+        if (sh_rows) gr.dsh = nullptr;  // deferred: the exchange writes dsh from the rows
         launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
                                  at<uint8_t>(g, GL.clamped), contrib, written, at<float4>(g, GL.rec),
-                                 at<float>(g, GL.shjac), *grads, st);
+                                 at<float>(g, GL.shjac), gr, sh_rows, st);
     }
     GSR_STAGE("gaussian backward");
     return 0;
 }
+}  // namespace
 
 size_t gsr_multiview_scratch_bytes(int P, int B) {
     return gsr::align_up(gsr::sh_rows_floats(P > 0 ? P : 0) * (size_t)(B > 0 ? B : 0) * 4) + gsr::ALIGN;
@@ -609,6 +646,40 @@ size_t gsr_multiview_scratch_bytes(int P, int B) {
 size_t gsr_sh_rows_floats(int P) { return gsr::sh_rows_floats(P > 0 ? P : 0); }
 
 namespace {
+// The multi-view backward alternates its views' render backwards between the caller's stream
+// and an auxiliary stream of libgsr's (one per device, created on first use), so that one
+// view's render backward fills the tail of the previous one instead of the chip idling half
+// empty behind the deepest tiles; the per-Gaussian pass waits for both.  The views write
+// disjoint scratch, and the caller's stream waits for the auxiliary one before anything that
+// follows, so the caller sees one stream's ordering.  gsr_set_option("mv_streams", 0) or a
+// debug call (stage-by-stage synchronisation) keeps everything on the caller's stream.
+struct AuxStream {
+    hipStream_t st = nullptr;
+};
+hipStream_t aux_stream() {
+    static std::mutex mu;
+    static AuxStream aux[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    if (!aux[dev].st && hipStreamCreateWithFlags(&aux[dev].st, hipStreamNonBlocking) != hipSuccess) aux[dev].st = nullptr;
+    return aux[dev].st;
+}
+// per thread and device: the fork and join events of one multi-view call (re-recorded by the
+// next call of the same thread only after this call enqueued its waits)
+struct ForkJoin {
+    hipEvent_t fork = nullptr, join = nullptr;
+};
+bool fork_join(ForkJoin*& fj) {
+    thread_local ForkJoin t[64];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return false;
+    fj = &t[dev];
+    if (!fj->fork && hipEventCreateWithFlags(&fj->fork, hipEventDisableTiming) != hipSuccess) return false;
+    if (!fj->join && hipEventCreateWithFlags(&fj->join, hipEventDisableTiming) != hipSuccess) return false;
+    return true;
+}
+
 int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs* in, void* mv_scratch,
                             float* sh_rows, const gsr_grads* grads, void* stream) {
     using namespace gsr;
@@ -632,6 +703,12 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
     if (in->shs && !mv_scratch && !defer) return fail("[gsr] multiview: scratch is NULL");
     hipStream_t st = (hipStream_t)stream;
     const bool dbg = s0->debug != 0;
+    hipStream_t aux = (B > 1 && g_mv_streams && !dbg) ? aux_stream() : nullptr;
+    ForkJoin* fj = nullptr;
+    if (aux && (!fork_join(fj) || hipEventRecord(fj->fork, st) != hipSuccess ||
+                hipStreamWaitEvent(aux, fj->fork, 0) != hipSuccess))
+        aux = nullptr;
+    bool aux_used = false;
     MvArgs a{};
     a.B = B;
     for (int v = 0; v < B; ++v) {
@@ -655,16 +732,18 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
             char* b = aligned_base(V.binning);
             contrib = reinterpret_cast<float*>(aligned_base(V.scratch));
             written = at<uint8_t>(b, BL.written);
+            const hipStream_t sv = (aux && (v & 1)) ? aux : st;  // odd views on the auxiliary stream
+            aux_used |= sv == aux;
             {
-                StageScope sc(GSR_STAGE_RENDER_BWD, st);
+                StageScope sc(GSR_STAGE_RENDER_BWD, sv);
                 launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order),
                                        at<uint32_t>(im, IL.order) + IL.gx * IL.gy, at<uint2>(im, IL.ranges),
                                        at<uint32_t>(b, BL.point_list),
                                        at<uint32_t>(b, BL.slot_vals), at<float4>(g, GL.rec), s->bg, V.alpha,
                                        at<uint32_t>(im, IL.n_contrib), V.dL_dcolor, V.dL_dsegment, V.dL_ddepth,
-                                       V.dL_dalpha, contrib, written, st);
+                                       V.dL_dalpha, contrib, written, sv);
             }
-            GSR_STAGE("render backward");
+            if (int rc = check("render backward", sv, dbg)) return rc;
         } else {
             // nothing rendered: every radius is 0 and the records are never read
             written = nullptr;
@@ -686,6 +765,13 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
         w.H = s->H;
         w.tanfovx = s->tanfovx;
         w.tanfovy = s->tanfovy;
+    }
+    if (aux) {  // join: the per-Gaussian pass (and the caller) after every view's render backward
+        if (!aux_used) {
+            // nothing went to the auxiliary stream (e.g. the odd views rendered nothing)
+        } else if (hipEventRecord(fj->join, aux) != hipSuccess || hipStreamWaitEvent(st, fj->join, 0) != hipSuccess) {
+            return fail("[gsr] multiview: stream join failed");
+        }
     }
     {
         StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);

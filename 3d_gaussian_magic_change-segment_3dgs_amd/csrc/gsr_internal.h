@@ -283,7 +283,7 @@ void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const 
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
                               const float* contrib, const uint8_t* written, const float4* rec,
-                              const float* shjac, const gsr_grads& g, hipStream_t st);
+                              const float* shjac, const gsr_grads& g, float* shx, hipStream_t st);
 // binning.hip
 // Optional last-pass outputs of a sort: ranges[key] = [first, last + 1) of each key's run in
 // the sorted order (atomicMin/atomicMax per run and tile; empty keys keep {~0u, 0}, which

@@ -580,7 +580,10 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
                                                            const float* __restrict__ contrib,
                                                            const uint8_t* __restrict__ written,
                                                            const float4* __restrict__ rec,
-                                                           const float* __restrict__ shjac, gsr_grads g) {
+                                                           const float* __restrict__ shjac, gsr_grads g,
+                                                           float* __restrict__ shx) {
+    // shx != NULL (gsr_backward_deferred_sh): the SH exchange rows of this view -- the
+    // clamped dRGB [P,3] and the camera centre -- instead of dsh (g.dsh is NULL then)
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     const int M = s.M;
     const size_t i3 = 3 * (size_t)idx;
@@ -624,6 +627,11 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
     float dc[3] = {0.f, 0.f, 0.f};
 #pragma unroll
     for (int i = 0; i < 16; ++i) bas[i] = 0.f;
+    if (shx && idx == 0) {
+        float* c = shx + sh_rows_campos(s.P);
+        c[0] = cam.campos.x; c[1] = cam.campos.y; c[2] = cam.campos.z; c[3] = 0.f;
+    }
+    if (shx && live && !vis) { shx[i3] = 0.f; shx[i3 + 1] = 0.f; shx[i3 + 2] = 0.f; }
     if (live && !vis) {
         // invisible: every gradient is zero (rasterize_points.cu:166-177 zero-init)
         if (g.dmeans2D) { g.dmeans2D[i3] = 0.f; g.dmeans2D[i3 + 1] = 0.f; g.dmeans2D[i3 + 2] = 0.f; }
@@ -757,6 +765,11 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
             dc[0] = dRGB.x;
             dc[1] = dRGB.y;
             dc[2] = dRGB.z;
+            if (shx) {  // the exchange row: the clamped colour gradient (k_gaussian_backward_mv's form)
+                shx[i3] = (cb & 1) ? 0.f : q[0];
+                shx[i3 + 1] = (cb & 2) ? 0.f : q[1];
+                shx[i3 + 2] = (cb & 4) ? 0.f : q[2];
+            }
             if (g.dsh && !stage_dsh) {
                 float* o = g.dsh + (size_t)idx * M * 3;
                 auto val = [&](int f) { return f < 48 ? bas[f / 3] * dc[f % 3] : 0.f; };
@@ -1096,7 +1109,6 @@ template <bool STAGED>
 __global__ void __launch_bounds__(256) k_sh_dsh(int P, int D, int M, const float* __restrict__ means3D, int V,
                                                 const float* __restrict__ shx, float* __restrict__ dsh) {
     const size_t chunk = sh_rows_floats(P);
-    __shared__ float rows[STAGED ? 4 : 1][STAGED ? 64 : 1][52];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int wbase = blockIdx.x * blockDim.x + wave * 64;
     const int idx = wbase + lane;
@@ -1122,18 +1134,28 @@ __global__ void __launch_bounds__(256) k_sh_dsh(int P, int D, int M, const float
         }
     }
     if (STAGED) {
-        float* row = rows[wave][lane];
+        // as k_gaussian_backward's dsh: per pass, 16 lanes park their rows (52-float pitch,
+        // conflict-free ds_write_b128) and the wave stores those 16 rows = 3 KB as 192
+        // consecutive float4s
+        __shared__ float4 srow[4][16][13];
 #pragma unroll
-        for (int i = 0; i < 12; ++i)
-            *reinterpret_cast<float4*>(row + 4 * i) = make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2],
-                                                                  acc[4 * i + 3]);
-        __syncthreads();
-        float4* dst = reinterpret_cast<float4*>(dsh + (size_t)wbase * 48);
+        for (int p = 0; p < 4; ++p) {
+            if ((lane >> 4) == p) {
+                float4* row = srow[wave][lane & 15];
 #pragma unroll
-        for (int r = 0; r < 12; ++r) {
-            const int f = lane + 64 * r;
-            const int rr = f / 12, col = f - 12 * (f / 12);
-            if (wbase + rr < P) dst[f] = *reinterpret_cast<const float4*>(&rows[wave][rr][4 * col]);
+                for (int i = 0; i < 12; ++i)
+                    row[i] = make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
+            }
+            __syncthreads();
+            const int g0 = wbase + 16 * p;
+            float4* dst = reinterpret_cast<float4*>(dsh + (size_t)g0 * 48);
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const int f = lane + 64 * r;
+                const int row = f / 12, col = f - 12 * (f / 12);
+                if (g0 + row < P) sh_st(dst + f, srow[wave][row][col]);
+            }
+            __syncthreads();
         }
     } else {
         float* o = dsh + (size_t)idx * M * 3;
@@ -1181,10 +1203,10 @@ void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const 
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
                               const float* contrib, const uint8_t* written, const float4* rec,
-                              const float* shjac, const gsr_grads& g, hipStream_t st) {
+                              const float* shjac, const gsr_grads& g, float* shx, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_gaussian_backward, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, radii, tiles_touched,
-                       goff, clamped, contrib, written, rec, shjac, g);
+                       goff, clamped, contrib, written, rec, shjac, g, in.shs ? shx : nullptr);
 }
 
 }  // namespace gsr

@@ -988,8 +988,11 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k
 }
 
 // No split (split_bwd_depth = 0): one wave per block and tile, deepest first.
+// 5 waves per SIMD (96 VGPRs): the compiler spills ~11 values that live across a batch,
+// reloaded once per batch, and the kernel runs 2.8% faster than at 4 waves without spills
+// (rocprofv3 kernel stats, profiles/round4_bwd_waves.txt)
 #ifndef GSR_BWD1_WAVES
-#define GSR_BWD1_WAVES 4
+#define GSR_BWD1_WAVES 5
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD1_WAVES))) k_render_bwd1(
     int W, int H, int gx, int T, uint32_t* __restrict__ sched,

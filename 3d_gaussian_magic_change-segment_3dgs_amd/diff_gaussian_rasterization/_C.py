@@ -71,6 +71,9 @@ GSR_NEED_BINNING = 2
 _lib.gsr_backward.restype = _i
 _lib.gsr_backward.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _vp, _vp, _vp, _vp, _i, _vp,
                               _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_Grads), _vp]
+if hasattr(_lib, "gsr_backward_deferred_sh"):  # (absent from builds older than round 4: A/B runs)
+    _lib.gsr_backward_deferred_sh.restype = _i
+    _lib.gsr_backward_deferred_sh.argtypes = _lib.gsr_backward.argtypes[:-1] + [_vp, _vp]
 _lib.gsr_mark_visible.restype = _i
 _lib.gsr_mark_visible.argtypes = [_i, _vp, _vp, _vp, _vp, _vp]
 _lib.gsr_last_error.restype = ctypes.c_char_p
@@ -123,7 +126,7 @@ EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_binning_capacity
                     "gsr_stream_copy",
                     "gsr_last_error", "gsr_version", "gsr_set_option", "gsr_multiview_scratch_bytes",
                     "gsr_backward_multiview", "gsr_sh_rows_floats", "gsr_backward_multiview_deferred_sh",
-                    "gsr_sh_backward")
+                    "gsr_sh_backward", "gsr_backward_deferred_sh")
 
 _DEBUG_FIELDS = {  # name -> (dtype, elements per unit, unit: P | I | T)
     "tiles_touched": (torch.int32, 1, "P"), "rec": (torch.float32, 16, "P"), "clamped": (torch.uint8, 1, "P"),
@@ -345,8 +348,11 @@ def grad_arena_layout(P, M):
 def rasterize_gaussians_backward(background, means3D, radii, colors, segments, scales, rotations, scale_modifier,
                                  cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, dL_dout_color,
                                  dL_dout_segment, dL_dout_depth, dL_dout_alpha, sh, degree, campos, geomBuffer, R,
-                                 binningBuffer, imageBuffer, alpha, debug):
+                                 binningBuffer, imageBuffer, alpha, debug, sh_rows=None):
     """RasterizeGaussiansBackwardCUDA (DGR/rasterize_points.cu:127-221).
+    sh_rows (fp32 tensor of sh_rows_floats(P) on the GPU, 16-B aligned): deferred SH mode
+    (gsr_backward_deferred_sh) -- this view's SH exchange rows are written there and the
+    returned dsh is left unwritten until sh_backward completes it.
     Returns (dL_dmeans2D, dL_dcolors, dL_dopacity, dL_dmeans3D, dL_dcov3D, dL_dsh, dL_dscales,
     dL_drotations, dL_dsegments).  Gradients of absent (empty) inputs are zero tensors of the
     reference's shapes ([P,3] / [P,6] / [P,0,3] / [P,3] / [P,4] / [P,2], rasterize_points.cu:
@@ -401,11 +407,20 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, segments, s
         g.dscales = dscales.data_ptr() if scales_ is not None else None
         g.drot = drot.data_ptr() if scales_ is not None else None
         g.dsegments = dsegments.data_ptr()
-        _check(_lib.gsr_backward(ctypes.byref(s), ctypes.byref(inp), radii_.data_ptr(), geomBuffer.data_ptr(),
-                                 binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(),
-                                 R, alpha_.data_ptr(), ups[0].data_ptr(), ups[1].data_ptr(), ups[2].data_ptr(),
-                                 ups[3].data_ptr(), scratch.data_ptr() if R > 0 else None, ctypes.byref(g),
-                                 _stream(device)))
+        bargs = (ctypes.byref(s), ctypes.byref(inp), radii_.data_ptr(), geomBuffer.data_ptr(),
+                 binningBuffer.data_ptr() if binningBuffer.numel() else None, imageBuffer.data_ptr(), R,
+                 alpha_.data_ptr(), ups[0].data_ptr(), ups[1].data_ptr(), ups[2].data_ptr(), ups[3].data_ptr(),
+                 scratch.data_ptr() if R > 0 else None, ctypes.byref(g))
+        if sh_rows is not None:
+            if sh_ is None:
+                raise RuntimeError("deferred SH backward: sh is required")
+            if (sh_rows.device != device or sh_rows.dtype != torch.float32 or not sh_rows.is_contiguous()
+                    or sh_rows.numel() < sh_rows_floats(P) or sh_rows.data_ptr() % 16):
+                raise RuntimeError("deferred SH backward: sh_rows must be a contiguous, 16-B aligned float32 "
+                                   f"tensor of sh_rows_floats(P) floats on {device}")
+            _check(_lib.gsr_backward_deferred_sh(*bargs, sh_rows.data_ptr(), _stream(device)))
+        else:
+            _check(_lib.gsr_backward(*bargs, _stream(device)))
     Z = lambda *shape: _zeros(device, *shape)
     return (dmeans2D, dcolors if colors_ is not None else Z(P, 3), dopacity, dmeans3D,
             dcov3D if cov_ is not None else Z(P, 6), dsh if sh_ is not None else Z(P, 0, 3),

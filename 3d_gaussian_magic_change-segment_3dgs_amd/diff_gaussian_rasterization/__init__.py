@@ -23,6 +23,8 @@ GaussianRasterizer with forward/markVisible (:182-235), rasterize_gaussians
 gaussian_renderer/__init__.py imports and calls it unchanged.  The compute path
 is libgsr.so (hand-written HIP for gfx950) through the ctypes module `_C`.
 """
+import contextlib
+import os
 import threading
 from typing import NamedTuple
 
@@ -45,8 +47,9 @@ class defer_sh_gradients:
     passes run inside it leave the SH gradient to a later exchange.  They write
     each view's SH exchange rows (include/gsr.h gsr_backward_multiview_deferred_sh)
     to a buffer obtained from `sink.sh_rows(B, P, device)` and report the call with
-    `sink.record(...)`; the returned dsh is NOT written yet and dmeans3D lacks the
-    SH direction term until the sink runs _C.sh_backward.  Calls without SH
+    `sink.record(...)`; the returned dsh is NOT written until the sink runs
+    _C.sh_backward (every other gradient, dmeans3D included, is complete; a single view
+    goes through gsr_backward_deferred_sh, several through the multi-view call).  Calls without SH
     coefficients (colors_precomp) are unaffected.  The context is process-wide (the
     autograd engine runs GPU backwards on its own threads).  An extension of the
     reference API."""
@@ -63,6 +66,18 @@ class defer_sh_gradients:
         with _SINKS_LOCK:
             _SINKS.remove(self.sink)
         return False
+
+
+# the multi-view forward's side stream per device (GSR_MV_STREAMS=0: one stream)
+_MV_STREAMS = os.environ.get("GSR_MV_STREAMS", "1") != "0"
+_VIEW_STREAMS = {}
+
+
+def _view_stream(device):
+    st = _VIEW_STREAMS.get(device)
+    if st is None:
+        st = _VIEW_STREAMS[device] = torch.cuda.Stream(device=device)
+    return st
 
 
 def _sh_sink():
@@ -199,17 +214,14 @@ class _RasterizeGaussians(torch.autograd.Function):
                 imgBuffer,
                 alpha,
                 raster_settings.debug)
-        if _sh_sink() is not None and sh.numel() > 0:
-            rs = raster_settings
-            view = {"bg": rs.bg, "viewmatrix": rs.viewmatrix, "projmatrix": rs.projmatrix, "tanfovx": rs.tanfovx,
-                    "tanfovy": rs.tanfovy, "image_height": rs.image_height, "image_width": rs.image_width,
-                    "campos": rs.campos, "radii": radii, "geom": geomBuffer, "binning": binningBuffer,
-                    "img": imgBuffer, "num_rendered": num_rendered, "alpha": alpha, "dL_dcolor": grad_color,
-                    "dL_dsegment": grad_segment, "dL_ddepth": grad_depth, "dL_dalpha": grad_alpha}
-            (_, g_col, g_op, g_m3, g_cov, g_sh, g_sc, g_rot, g_seg), d2 = _backward_views(
-                [view], means3D, colors_precomp, segments, scales, rotations, rs.scale_modifier, cov3Ds_precomp, sh,
-                rs.sh_degree, rs.debug)
-            out = (d2[0], g_col, g_op, g_m3, g_cov, g_sh, g_sc, g_rot, g_seg)
+        sink = _sh_sink() if sh.numel() > 0 else None
+        if sink is not None:
+            # deferred SH (view-parallel exchange): the single-view backward writes this view's
+            # exchange rows instead of dsh (include/gsr.h gsr_backward_deferred_sh)
+            rows = sink.sh_rows(1, int(means3D.size(0)), means3D.device)
+            out = _C.rasterize_gaussians_backward(*args, sh_rows=rows)
+            sink.record(rows, 1, means3D, sh, raster_settings.sh_degree, out[5], out[3],
+                        inputs=tuple(t for t in (segments, scales, rotations) if isinstance(t, torch.Tensor)))
         elif raster_settings.debug:
             cpu_args = cpu_deep_copy_tuple(args)
             try:
@@ -260,16 +272,34 @@ class _RasterizeGaussiansMultiview(torch.autograd.Function):
     @staticmethod
     def forward(ctx, means3D, sh, colors_precomp, segments, opacities, scales, rotations, cov3Ds_precomp,
                 settings_list, *means2D_list):
+        # Views alternate between the caller's stream and a side stream, so that view v+1's
+        # preprocess and binning (short, latency-bound launches) run beside view v's render
+        # tail; the caller's stream then waits for the side stream.  Tensors made on the side
+        # stream are recorded on the caller's (caching-allocator rule for cross-stream use).
         outs, views = [], []
-        for rs in settings_list:
-            out = _C.rasterize_gaussians(rs.bg, means3D, colors_precomp, segments, opacities, scales, rotations,
-                                         rs.scale_modifier, cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx,
-                                         rs.tanfovy, rs.image_height, rs.image_width, sh, rs.sh_degree, rs.campos,
-                                         rs.prefiltered, rs.debug)
+        dev = means3D.device
+        main = torch.cuda.current_stream(dev) if means3D.is_cuda else None
+        side = _view_stream(dev) if (main is not None and len(settings_list) > 1 and _MV_STREAMS
+                                     and not any(rs.debug for rs in settings_list)) else None
+        if side is not None:
+            side.wait_stream(main)
+        for v, rs in enumerate(settings_list):
+            on_side = side is not None and (v & 1) == 1
+            with torch.cuda.stream(side) if on_side else contextlib.nullcontext():
+                out = _C.rasterize_gaussians(rs.bg, means3D, colors_precomp, segments, opacities, scales,
+                                             rotations, rs.scale_modifier, cov3Ds_precomp, rs.viewmatrix,
+                                             rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
+                                             rs.image_width, sh, rs.sh_degree, rs.campos, rs.prefiltered, rs.debug)
             num_rendered, color, depth, segment, alpha, radii, geom, binning, img = out
+            if on_side:
+                for t in (color, depth, segment, alpha, radii, geom, binning, img):
+                    if t.is_cuda and t.numel() > 0:
+                        t.record_stream(main)
             views.append((num_rendered, radii, geom, binning, img, alpha))
             ctx.mark_non_differentiable(radii)
             outs += [color, radii, depth, alpha, segment]
+        if side is not None:
+            main.wait_stream(side)
         ctx.settings_list = settings_list
         ctx.views = views
         ctx.save_for_backward(colors_precomp, segments, means3D, scales, rotations, cov3Ds_precomp, sh)

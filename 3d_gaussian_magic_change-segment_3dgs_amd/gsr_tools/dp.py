@@ -17,8 +17,14 @@ Two exchanges give the same summed bucket:
     ShExchange 2(N-1)/N*52 + (N-1)*B*12 B -- 3.8x less at N=2, 2.4x at N=8 (B=1).
     choose_exchange() picks the cheaper one.
 """
+import os
+import time
+
 import torch
 import torch.distributed as dist
+
+# GSR_HOST_PROFILE=1: host seconds spent in ShExchange.start's phases (bench.py reports them)
+HOST_TIMES = {} if os.environ.get("GSR_HOST_PROFILE") == "1" else None
 
 
 def arena_layout(P, M):
@@ -239,6 +245,7 @@ class ShExchange:
         return _ShExchangeHandle([self._start_one(e) for e in entries])
 
     def _start_one(self, e):
+        t0 = time.perf_counter() if HOST_TIMES is not None else 0.0
         P, M = e["P"], e["M"]
         lay = arena_layout(P, M)
         arena, rows = e["arena"], e["rows"]
@@ -250,9 +257,13 @@ class ShExchange:
         rest = arena.narrow(0, o_rest, lay["bucket"][1] - o_rest)
         rows_all = torch.empty(world * rows.numel(), dtype=rows.dtype, device=rows.device)
         cuda = rows.is_cuda
+        # (torch's _coalescing_manager around these three left rows_all unfilled on RCCL at
+        # world size 1 -- tests/test_gpu_dist.py caught it: three calls)
+        t1 = time.perf_counter() if HOST_TIMES is not None else 0.0
         works = [dist.all_reduce(xyz, op=dist.ReduceOp.SUM, group=self.group, async_op=True),
                  dist.all_reduce(rest, op=dist.ReduceOp.SUM, group=self.group, async_op=True),
                  _all_gather_flat(rows_all, rows, self.group, True)]
+        t2 = time.perf_counter() if HOST_TIMES is not None else 0.0
         V = world * e["B"]
         fn = self._sh_backward
         if fn is None:
@@ -271,8 +282,14 @@ class ShExchange:
             fn(rows_all, V, e["means3D"], e["sh"], e["degree"], dsh, dmeans3D)
             ev = torch.cuda.Event()
             ev.record(side)
-        for t in keep:
-            t.record_stream(side)
+        if HOST_TIMES is not None:
+            t3 = time.perf_counter()
+            for k, v in (("views", t1 - t0), ("collectives", t2 - t1), ("side_stream", t3 - t2)):
+                HOST_TIMES[k] = HOST_TIMES.get(k, 0.0) + v
+            HOST_TIMES["n"] = HOST_TIMES.get("n", 0) + 1
+        # `keep` holds every tensor the side stream touches until wait() has ordered the
+        # caller's stream after it (no record_stream per tensor: the handle must be waited,
+        # and an unwaited handle waits when it is dropped)
         return (ev, keep, e)
 
 
@@ -290,10 +307,21 @@ class _ShExchangeHandle:
         self.parts = parts
 
     def wait(self):
-        for ev, _, e in self.parts:
+        parts, self.parts = self.parts, []
+        for ev, _, e in parts:
             if ev is not None:
                 torch.cuda.current_stream().wait_event(ev)
             _check_leaf_grads(e)
+
+    def __del__(self):
+        # dropped without wait(): order the current stream after the side stream before the
+        # tensors it still uses go back to the caching allocator
+        for ev, _, _ in getattr(self, "parts", []):
+            if ev is not None:
+                try:
+                    torch.cuda.current_stream().wait_event(ev)
+                except Exception:
+                    pass
         self.parts = []
 
 

@@ -305,6 +305,9 @@ def main():
     up_list = [ups["color"], ups["depth"], ups["alpha"], ups["segment"]]
 
     pending = []  # the exchange in flight: (work handle, gradients kept alive)
+    # GSR_HOST_PROFILE=1: host seconds per step spent launching the view and the exchange
+    HOST_PROFILE = os.environ.get("GSR_HOST_PROFILE") == "1"
+    host_times = {"fwd+bwd": 0.0, "exchange": 0.0, "n": 0}
 
     def exchange_kind(nv):
         """The exchange for nv views per rank and its modelled cost (dp.exchange_cost), with the
@@ -339,10 +342,16 @@ def main():
         kind, model = exchange_kind(nv)
 
         def step():
+            t0 = time.perf_counter()
             ex = dp.ShExchange() if kind == "sh" else None
             with dgr.defer_sh_gradients(ex) if ex is not None else contextlib.nullcontext():
                 g = grads_of_views()
+            t1 = time.perf_counter()
             exchange(g, ex)
+            if HOST_PROFILE:
+                host_times["fwd+bwd"] += t1 - t0
+                host_times["exchange"] += time.perf_counter() - t1
+                host_times["n"] += 1
             return g
 
         def grads_of_views():
@@ -380,6 +389,10 @@ def main():
         once per window rather than every step."""
         nw = k // stride
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(nw + 1)] if per_step is not None else None
+        if HOST_PROFILE:  # host times of the timed steps only
+            host_times.update({"fwd+bwd": 0.0, "exchange": 0.0, "n": 0})
+            if dp.HOST_TIMES is not None:
+                dp.HOST_TIMES.clear()
         gc.disable()
         if dist is not None:
             dist.barrier()
@@ -517,6 +530,12 @@ def main():
                                f"{dp.LINK_GBPS:g} GB/s x {dp.LINK_EFF:g} (assumed), HBM work at {dp.HBM_GBPS:g} GB/s, "
                                "the SH rebuild timed on this GPU"} if dist is not None else None),
     }
+    if HOST_PROFILE and host_times["n"]:
+        n = host_times["n"]
+        out["host_us_per_step"] = {k: round(1e6 * v / n, 1) for k, v in host_times.items() if k != "n"}
+        if dp.HOST_TIMES and dp.HOST_TIMES.get("n"):
+            out["host_us_per_step"]["sh_exchange_start"] = {k: round(1e6 * v / dp.HOST_TIMES["n"], 1)
+                                                            for k, v in dp.HOST_TIMES.items() if k != "n"}
     out["batched"] = None
     if BB > 1 and BB != B:
         # The same hot path with a batch of BB views per rank per step: per-view forward,

@@ -219,6 +219,16 @@ GSR_API int gsr_backward_multiview(int B, const gsr_view_state* views, const gsr
  * dmeans3D are accepted for ABI compatibility and not used (shs may be NULL).  Run on
  * the all-gathered rows, the result equals the all-reduce of the complete dsh. */
 GSR_API size_t gsr_sh_rows_floats(int P);
+/* gsr_backward_deferred_sh: gsr_backward (shs required) that writes this view's rows to
+ * sh_rows [gsr_sh_rows_floats(P)] (16-B aligned) instead of grads->dsh (left unwritten);
+ * every other gradient, dmeans3D included, is complete.  One view per rank and step needs
+ * no multi-view call: this is the single-view backward with 12 B of rows written in place
+ * of the 192-B dsh rows. */
+GSR_API int gsr_backward_deferred_sh(const gsr_settings* s, const gsr_inputs* in, const int* radii, void* geom,
+                                     void* binning, void* img, int num_rendered, const float* alpha,
+                                     const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
+                                     const float* dL_dalpha, void* scratch, const gsr_grads* grads, float* sh_rows,
+                                     void* stream);
 GSR_API int gsr_backward_multiview_deferred_sh(int B, const gsr_view_state* views, const gsr_inputs* in,
                                                float* sh_rows, const gsr_grads* grads, void* stream);
 GSR_API int gsr_sh_backward(int V, int P, int D, int M, const float* shs, const float* means3D,

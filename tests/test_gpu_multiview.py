@@ -231,3 +231,34 @@ def test_sh_exchange_single_rank_equals_dropin(gpu_available):
     for k, r in ref.items():
         err = float((got[k] - r).norm() / max(float(r.norm()), 1e-30))
         assert err <= 1e-6, f"{k}: normwise error {err:.2e}"
+
+
+def test_deferred_sh_single_view_completes_to_dropin(gpu_available):
+    """gsr_backward_deferred_sh (one view per rank: the single-view backward writing its
+    exchange rows instead of dsh) completed by sh_backward gives the drop-in single-view
+    gradients bit for bit: dmeans3D carries the direction term already, dsh is rebuilt from
+    the row with the same basis products."""
+    from diff_gaussian_rasterization import _C, defer_sh_gradients, rasterize_gaussians
+    scene = synthetic_scene(5000, sh_degree=3, seed=50)
+    d = _leaves(scene)
+    (st, ups), = _views(1, 3)
+
+    def run():
+        m2 = torch.zeros_like(d["means3D"], requires_grad=True)
+        color, radii, depth, alpha, seg = rasterize_gaussians(d["means3D"], m2, raster_settings=st, **_kw(d))
+        return torch.autograd.grad([color, depth, alpha, seg], [d[k] for k in d] + [m2],
+                                   [ups["color"].to(DEV), ups["depth"].to(DEV), ups["alpha"].to(DEV),
+                                    ups["segment"].to(DEV)])
+
+    ref = run()
+    sink = _Sink()
+    with defer_sh_gradients(sink):
+        got = run()
+    assert len(sink.entries) == 1
+    rows, B, means3D, sh, degree, dsh, dmeans3D = sink.entries[0]
+    assert B == 1 and dsh.data_ptr() == got[list(d).index("shs")].data_ptr()
+    ch = _C.sh_rows_floats(scene.P)
+    assert torch.equal(rows[ch - 64:ch - 61], st.campos.float())
+    _C.sh_backward(rows, 1, means3D.detach(), sh.detach(), degree, dsh, dmeans3D)
+    for k, a, b in zip(list(d) + ["means2D"], got, ref):
+        assert torch.equal(a, b), f"{k} differs after the SH completion"

@@ -7,6 +7,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 mkdir -p gpurun_out/rccl
 STEPS=${STEPS:-100}
+export GSR_HOST_PROFILE=1
 timeout -k 10 300 python bench.py --steps $STEPS --warmup 10 --no-cpu-baseline --no-train --batched-views 1 \
   > gpurun_out/rccl/none.json 2> gpurun_out/rccl/none.err || { tail -20 gpurun_out/rccl/none.err; exit 1; }
 for ex in sh allreduce; do
@@ -20,6 +21,6 @@ import json
 for m in ("none", "sh", "allreduce"):
     d = json.load(open(f"gpurun_out/rccl/{m}.json"))
     ex = d.get("exchange") or {}
-    print(m, d["value"], d["ms_per_step"], d["config"].get("dist_backend"), ex.get("chosen"),
+    print(m, d["value"], d["ms_per_step"], d["config"].get("dist_backend"), ex.get("chosen"), d.get("host_us_per_step"),
           json.dumps(ex.get("model_us")))
 PY
