@@ -869,6 +869,7 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
     else if (n == "goff") G(GL.goff, Pz * 4);
     else if (n == "point_list") B(BL.point_list, I * 4);
     else if (n == "slot_vals") B(BL.slot_vals, I * 4);
+    else if (n == "written") B(BL.written, I);  // the backward's written-record flags (1 byte per slot)
     else if (n == "ranges") M(IL.ranges, T * 8);
     else if (n == "n_contrib_tiles") M(IL.n_contrib, T * TILE_PIX * 4);
     else if (n == "tile_order") M(IL.order, tile_sched_words(T) * 4);  // heavy-first order + TileSched

@@ -145,6 +145,20 @@ __device__ __forceinline__ M3 vrk_of(const float* c) {
 #define GSR_NT_SH_STORE
 #endif
 typedef float sh_v4 __attribute__((ext_vector_type(4)));
+// The SH-row staging below is per wave (each wave parks and reads back only its own LDS rows),
+// so a wave-level LDS fence replaces the block barriers: a wave's LDS instructions execute in
+// order, so waiting for its own outstanding LDS operations (and keeping the compiler from moving
+// LDS accesses across the point) orders its writes before its reads and its reads before the next
+// pass's writes.  Without block barriers the four waves of a block no longer wait for each other
+// at every pass, so their loads overlap more.
+__device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+
+#ifdef GSR_BLOCK_SYNC  // (A/B: the block barriers the fence replaced)
+#define GSR_WAVE_SYNC() __syncthreads()
+#else
+#define GSR_WAVE_SYNC() wave_lds_fence()
+#endif
+
 __device__ __forceinline__ float4 sh_ld(const float4* p) {
 #ifdef GSR_NT_SH_LOAD
     const sh_v4 r = __builtin_nontemporal_load(reinterpret_cast<const sh_v4*>(p));
@@ -421,7 +435,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
                     const int row = f / 12, col = f - 12 * (f / 12);
                     *reinterpret_cast<float4*>(&shrow[wave][row][4 * col]) = shv[r];
                 }
-                __syncthreads();
+                GSR_WAVE_SYNC();
                 if ((lane >> 5) == h && ok) {
                     const float* S = shrow[wave][lane & 31];
                     auto Sf = [&](int i) { return f3{S[3 * i], S[3 * i + 1], S[3 * i + 2]}; };
@@ -432,7 +446,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
                         store_jac(jx, jy, jz);
                     }
                 }
-                __syncthreads();
+                GSR_WAVE_SYNC();
             }
         } else if (ok) {
             // per-coefficient loads: here they overlap the projection math better than a
@@ -858,7 +872,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
                 for (int i = 0; i < 12; ++i)
                     row[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
             }
-            __syncthreads();
+            GSR_WAVE_SYNC();
             const int g0 = wbase + 16 * p;
             float4* dst = reinterpret_cast<float4*>(g.dsh + (size_t)g0 * 48);
 #pragma unroll
@@ -867,7 +881,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
                 const int row = f / 12, col = f - 12 * (f / 12);
                 if (g0 + row < s.P) sh_st(dst + f, srow[wave][row][col]);
             }
-            __syncthreads();
+            GSR_WAVE_SYNC();
         }
     }
 }
@@ -1146,7 +1160,7 @@ __global__ void __launch_bounds__(256) k_sh_dsh(int P, int D, int M, const float
                 for (int i = 0; i < 12; ++i)
                     row[i] = make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
             }
-            __syncthreads();
+            GSR_WAVE_SYNC();
             const int g0 = wbase + 16 * p;
             float4* dst = reinterpret_cast<float4*>(dsh + (size_t)g0 * 48);
 #pragma unroll
@@ -1155,7 +1169,7 @@ __global__ void __launch_bounds__(256) k_sh_dsh(int P, int D, int M, const float
                 const int row = f / 12, col = f - 12 * (f / 12);
                 if (g0 + row < P) sh_st(dst + f, srow[wave][row][col]);
             }
-            __syncthreads();
+            GSR_WAVE_SYNC();
         }
     } else {
         float* o = dsh + (size_t)idx * M * 3;

@@ -132,6 +132,7 @@ _DEBUG_FIELDS = {  # name -> (dtype, elements per unit, unit: P | I | T)
     "tiles_touched": (torch.int32, 1, "P"), "rec": (torch.float32, 16, "P"), "clamped": (torch.uint8, 1, "P"),
     "order": (torch.int32, 1, "P"), "goff": (torch.int32, 1, "P"), "point_list": (torch.int32, 1, "I"),
     "slot_vals": (torch.int32, 1, "I"), "ranges": (torch.int32, 2, "T"), "n_contrib_tiles": (torch.int32, 256, "T"),
+    "written": (torch.uint8, 1, "I"),  # after a backward: 1 where the render backward stored a record
     "tile_order": (torch.int32, 1, "T+"),  # heavy-first tile order + the render schedule (gsr_internal.h TileSched)
 }
 

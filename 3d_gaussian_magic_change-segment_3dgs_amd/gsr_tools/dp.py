@@ -234,7 +234,11 @@ class ShExchange:
                 seen.add(id(t))
                 gr = t.grad
                 watch.append((t, gr, None if gr is None else gr._version))
-        self.entries.append(dict(rows=rows, B=B, means3D=means3D.detach(), sh=sh.detach(), degree=int(degree),
+        m3 = means3D.detach()
+        if m3.is_cuda and (m3.dtype != torch.float32 or not m3.is_contiguous() or rows.device != m3.device or
+                           rows.dtype != torch.float32 or not rows.is_contiguous()):
+            raise RuntimeError("ShExchange: means3D and the rows must be contiguous float32 tensors on one device")
+        self.entries.append(dict(rows=rows, B=B, means3D=m3, sh=sh.detach(), degree=int(degree),
                                  arena=arena, P=P, M=M, watch=watch))
 
     def start(self):
@@ -249,8 +253,6 @@ class ShExchange:
         P, M = e["P"], e["M"]
         lay = arena_layout(P, M)
         arena, rows = e["arena"], e["rows"]
-        dsh = arena.narrow(0, lay["dsh"][0], 3 * M * P).view(P, M, 3)
-        dmeans3D = arena.narrow(0, lay["dmeans3D"][0], 3 * P).view(P, 3)
         world = dist.get_world_size(self.group)
         xyz = arena.narrow(0, lay["dmeans3D"][0], 3 * P)
         o_rest = lay["dopacity"][0]
@@ -266,12 +268,12 @@ class ShExchange:
         t2 = time.perf_counter() if HOST_TIMES is not None else 0.0
         V = world * e["B"]
         fn = self._sh_backward
-        if fn is None:
-            from diff_gaussian_rasterization._C import sh_backward as fn
         keep = (arena, rows, rows_all, e["means3D"], e["sh"])
         if not cuda:
             for w in works:
                 w.wait()
+            dsh = arena.narrow(0, lay["dsh"][0], 3 * M * P).view(P, M, 3)
+            dmeans3D = arena.narrow(0, lay["dmeans3D"][0], 3 * P).view(P, 3)
             fn(rows_all, V, e["means3D"], e["sh"], e["degree"], dsh, dmeans3D)
             return (None, keep, e)
         side = _side_stream(rows.device)
@@ -279,7 +281,17 @@ class ShExchange:
         with torch.cuda.stream(side):
             for w in works:
                 w.wait()  # stream-side wait on the collective
-            fn(rows_all, V, e["means3D"], e["sh"], e["degree"], dsh, dmeans3D)
+            if fn is None:
+                # gsr_sh_backward straight through ctypes: the tensors were checked when the
+                # backward made them (record), and dsh is the arena's dsh block
+                from diff_gaussian_rasterization import _C
+                _C._check(_C._lib.gsr_sh_backward(V, P, e["degree"], M, None, e["means3D"].data_ptr(),
+                                                  rows_all.data_ptr(), arena.data_ptr() + 4 * lay["dsh"][0], None,
+                                                  side.cuda_stream))
+            else:
+                dsh = arena.narrow(0, lay["dsh"][0], 3 * M * P).view(P, M, 3)
+                dmeans3D = arena.narrow(0, lay["dmeans3D"][0], 3 * P).view(P, 3)
+                fn(rows_all, V, e["means3D"], e["sh"], e["degree"], dsh, dmeans3D)
             ev = torch.cuda.Event()
             ev.record(side)
         if HOST_TIMES is not None:

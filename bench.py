@@ -99,7 +99,7 @@ def dist_info(dist):
             "collective_lib": "RCCL" if backend == "nccl" else backend, "rccl_version": ver}
 
 
-def algorithmic_bytes(stage, P, I, HW, deg, views=1, T=0):
+def algorithmic_bytes(stage, P, I, HW, deg, views=1, T=0, written=None):
     """Bytes a stage must move per launch: SURVEY.md s8(d)'s per-unit figures
     (a7..a16) attributed to the gsr stage that does that work."""
     M = (deg + 1) ** 2
@@ -119,8 +119,16 @@ def algorithmic_bytes(stage, P, I, HW, deg, views=1, T=0):
         return 52 * I + 32 * HW
     if stage == "render_bwd":      # a14 (per-instance + per-pixel part)
         return 52 * I + 36 * HW
-    if stage == "gaussian_bwd":    # a14 grad outs + a15 + a16: 56 + 92 + (151 + 24 M) B per Gaussian and view
-        return (56 + 92 + 151 + 24 * M) * P * views
+    if stage == "gaussian_bwd":
+        # the fused kernel's own minimal bytes (SURVEY's a14 + a15 + a16 figure,
+        # (299 + 24 M) B, assumes separate launches that re-read the SH rows and pass dL_dmean3D /
+        # dL_dcov3D through memory, and came out above the copy rate at 6M Gaussians).  Per
+        # Gaussian and view: radii, goff, tiles_touched, the 32-B half record, means3D, rotation,
+        # scale, clamp byte and the 36-B SH direction Jacobian read (121 B); dmeans2D, dopacity,
+        # dmeans3D, dscales, drot, dsegments and the 12 M-float dsh row written (64 + 12 M B).
+        # Per instance: its written flag (1 B); per written record: 48 B (W, measured).
+        W = written if written is not None else I
+        return ((121 + 64 + 12 * M) * P + I + 48 * W) * views
     return 0
 
 
@@ -309,7 +317,7 @@ def main():
     HOST_PROFILE = os.environ.get("GSR_HOST_PROFILE") == "1"
     host_times = {"fwd+bwd": 0.0, "exchange": 0.0, "n": 0}
 
-    def exchange_kind(nv):
+    def exchange_kind(nv, force=None):
         """The exchange for nv views per rank and its modelled cost (dp.exchange_cost), with the
         SH exchange's dsh rebuild timed on this GPU at the step's view count (world * nv rows)."""
         if dist is None:
@@ -317,7 +325,8 @@ def main():
         M = shs.shape[1]
         rb = dp.measure_rebuild_us(P, M, world * nv, device, degree=deg)
         model = dp.exchange_cost(world, nv, P, M, rebuild_us=rb)
-        kind = dp.choose_exchange(world, nv, M, P=P, rebuild_us=rb) if args.exchange == "auto" else args.exchange
+        kind = force or (dp.choose_exchange(world, nv, M, P=P, rebuild_us=rb) if args.exchange == "auto"
+                         else args.exchange)
         return kind, model
 
     def exchange(g, ex=None):
@@ -338,8 +347,8 @@ def main():
         while pending:
             pending.pop()[0].wait()
 
-    def make_step(nv):
-        kind, model = exchange_kind(nv)
+    def make_step(nv, force=None):
+        kind, model = exchange_kind(nv, force)
 
         def step():
             t0 = time.perf_counter()
@@ -375,6 +384,20 @@ def main():
         return step
 
     step = make_step(B)
+
+    def written_records():
+        """Instance slots the render backward stores a gradient record for, in one view (view 0)
+        through the private bindings (outside any timed region): the per-record term of
+        gaussian_bwd's algorithmic bytes."""
+        rs = settings[0]
+        out = _C.rasterize_gaussians(rs.bg, means3D, E, segs, opac, scales, rots, 1.0, E, rs.viewmatrix,
+                                     rs.projmatrix, rs.tanfovx, rs.tanfovy, H, W, shs, deg, rs.campos, False, False)
+        R, _, _, _, alpha, radii, geom, binning, img = out
+        _C.rasterize_gaussians_backward(rs.bg, means3D, radii, E, segs, scales, rots, 1.0, E, rs.viewmatrix,
+                                        rs.projmatrix, rs.tanfovx, rs.tanfovy, ups["color"], ups["segment"],
+                                        ups["depth"], ups["alpha"], shs, deg, rs.campos, geom, R, binning, img,
+                                        alpha, False)
+        return int(_C.debug_state("written", P, W, H, R, geom, binning, img).sum()) if R > 0 else 0
 
     def timed(fn, k, per_step=None, stride=1, dom_mask=0):
         """k steps between a barrier + device sync on both sides; max over ranks.  Python's
@@ -424,6 +447,23 @@ def main():
         step()
     drain()
     torch.cuda.synchronize()
+    if dist is not None and args.exchange == "auto" and step.exchange is not None:
+        # The measured choice: the model (dp.exchange_cost) prices link bytes, HBM work and the
+        # timed SH rebuild, but not the host's launch work per exchange, which can leave the GPU
+        # idle between steps.  A few steps of each exchange (max over ranks) decide.
+        modelled = step.exchange
+        cand = {modelled: step}
+        other = "allreduce" if modelled == "sh" else "sh"
+        cand[other] = make_step(B, force=other)
+        trial = {}
+        for kind, fn in cand.items():
+            for _ in range(3):
+                fn()
+            drain()
+            trial[kind] = timed(fn, 8) / 8
+        step = cand[min(trial, key=trial.get)]
+        step.exchange_trial_ms = {k: round(1e3 * v, 4) for k, v in trial.items()}
+        step.exchange_modelled = modelled
     nst = _C._lib.gsr_num_stages()
     import ctypes
     names = [_C._lib.gsr_stage_name(i).decode() for i in range(nst)]
@@ -455,13 +495,15 @@ def main():
     _C._lib.gsr_timing_enable(0)
     ms, cnt = collect()  # the dominant stage's launches inside the timed region
     I, HW = int(state["I"]), W * H
+    Wrec = written_records()  # gradient records the render backward stores (gaussian_bwd's bytes)
     stages = {}
     for i in range(nst):
         if scnt[i]:
             avg = sms[i] / scnt[i]
             stages[names[i]] = {"avg_ms": round(avg, 4), "ms_per_step": round(sms[i] / n_stage_steps, 4),
                                 "launches_per_step": scnt[i] / n_stage_steps,
-                                "gbs": round(algorithmic_bytes(names[i], P, I, HW, deg, B, T=((W + 15) // 16) * ((H + 15) // 16))
+                                "gbs": round(algorithmic_bytes(names[i], P, I, HW, deg, B, T=((W + 15) // 16) * ((H + 15) // 16),
+                                                               written=Wrec)
                                              / (avg * 1e-3) / 1e9, 1)}
     dom = names[dom_i] if stages else None
     dinfo = dist_info(dist)
@@ -469,7 +511,7 @@ def main():
     roof = None
     if dom and cnt[dom_i]:
         avg_live = ms[dom_i] / cnt[dom_i]  # measured inside the timed region
-        achieved = round(algorithmic_bytes(dom, P, I, HW, deg, B) / (avg_live * 1e-3) / 1e9, 1)
+        achieved = round(algorithmic_bytes(dom, P, I, HW, deg, B, written=Wrec) / (avg_live * 1e-3) / 1e9, 1)
         traffic = cyc_per_valu = None
         pmc, pmc_note = pmc_for_this_build()
         if pmc is not None:
@@ -489,7 +531,7 @@ def main():
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "measured_copy_peak": measured_peak,
                 "frac_of_measured_peak": round(achieved / measured_peak, 4) if measured_peak else None,
-                "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg, B),
+                "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg, B, written=Wrec),
                 "avg_launch_ms": round(avg_live, 4), "launches_timed": int(cnt[dom_i]),
                 "valu_instr_per_launch": (pmc.get("kernels", {}).get(dom, {}).get("SQ_INSTS_VALU")
                                           if pmc is not None else None),
@@ -516,7 +558,7 @@ def main():
         "config": {"workload": f"{args.config}: P={P} Gaussians, SH{deg}, {W}x{H}, fwd+bwd per view; {B} view(s) per "
                                f"rank per step" + (" (per-view forward, one multi-view backward)" if B > 1 else
                                                    " through the drop-in GaussianRasterizer"), "P": P, "width": W, "height": H, "sh_degree": deg,
-                   "num_classes": 2, "num_rendered": I, "global_batch": world * B, "views_per_step_per_gpu": B,
+                   "num_classes": 2, "num_rendered": I, "written_records": Wrec, "global_batch": world * B, "views_per_step_per_gpu": B,
                    "parallelism": f"dp{world}" + ((" (views sharded; " +
                                                    EXCHANGE_DESC[step.exchange].format(lib=dinfo["collective_lib"]) +
                                                    " per step, overlapped with the next step's render)")
@@ -526,6 +568,8 @@ def main():
         "roofline": roof,
         "stages": stages,
         "exchange": ({"chosen": step.exchange, "mode": args.exchange, "model_us": step.exchange_model,
+                      "modelled_choice": getattr(step, "exchange_modelled", None),
+                      "trial_ms_per_step": getattr(step, "exchange_trial_ms", None),
                       "model": "gsr_tools/dp.py exchange_cost: ring bytes over world-1 xGMI links at "
                                f"{dp.LINK_GBPS:g} GB/s x {dp.LINK_EFF:g} (assumed), HBM work at {dp.HBM_GBPS:g} GB/s, "
                                "the SH rebuild timed on this GPU"} if dist is not None else None),

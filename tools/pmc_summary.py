@@ -7,7 +7,7 @@ import csv, glob, json, os, sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PMC = os.path.join(ROOT, "gpurun_out", "pmc")
+PMC = os.environ.get("GSR_PMC_DIR", os.path.join(ROOT, "gpurun_out", "pmc"))  # (tools/pmc_cfg.sh: gpurun_out/pmc_CONFIG)
 STAGE_OF = {"k_render_bwd": "render_bwd", "k_render_bwd1": "render_bwd", "k_render_fwd": "render_fwd", "k_gaussian_backward": "gaussian_bwd",
             "k_preprocess": "preprocess", "k_duplicate": "duplicate", "k_tile_order": "ranges", "k_tile_order_counted": "ranges", "k_scan": "scan", "k_radix_hist": "radix_hist",
             "k_radix_scatter": "radix_scatter", "k_radix_upsweep": "radix_upsweep", "k_adam": "adam_step",
