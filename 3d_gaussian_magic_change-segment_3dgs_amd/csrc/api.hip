@@ -291,6 +291,10 @@ int gsr_set_option(const char* name, long long value) {
         gsr::set_split_buckets(gsr::split_fwd_bucket(), (int)value);
         return 0;
     }
+    if (std::string(name) == "bwd_ckpt") {  // render backward list segments at this position (x64); 0 = off
+        gsr::set_bwd_ckpt((int)value);
+        return 0;
+    }
     if (std::string(name) == "sort_grouped") {  // depth sort: grouped look-back passes (default on)
         gsr::set_sort_grouped(value != 0);
         return 0;
@@ -525,7 +529,7 @@ int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* b
         StageScope sc(GSR_STAGE_RENDER_FWD, st);
         launch_render_forward(s->W, s->H, IL.gx, IL.gy, order, order + T, ranges, point_list,
                               g ? at<float4>(g, GL.rec) : nullptr, s->bg, out_color, out_depth, out_alpha,
-                              out_segment, at<uint32_t>(im, IL.n_contrib), st);
+                              out_segment, at<uint32_t>(im, IL.n_contrib), at<float>(im, IL.ckpt), st);
     }
     GSR_STAGE("render");
     return 0;
@@ -622,7 +626,7 @@ int backward_impl(const gsr_settings* s, const gsr_inputs* in, const int* radii,
                                    at<uint32_t>(im, IL.order) + IL.gx * IL.gy, at<uint2>(im, IL.ranges),
                                    at<uint32_t>(b, BL.point_list), at<uint32_t>(b, BL.slot_vals),
                                    at<float4>(g, GL.rec), s->bg, alpha, at<uint32_t>(im, IL.n_contrib), dL_dcolor,
-                                   dL_dsegment, dL_ddepth, dL_dalpha, contrib, written, st);
+                                   dL_dsegment, dL_ddepth, dL_dalpha, contrib, written, at<float>(im, IL.ckpt), st);
         }
         GSR_STAGE("render backward");
     }
@@ -741,7 +745,7 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
                                        at<uint32_t>(b, BL.point_list),
                                        at<uint32_t>(b, BL.slot_vals), at<float4>(g, GL.rec), s->bg, V.alpha,
                                        at<uint32_t>(im, IL.n_contrib), V.dL_dcolor, V.dL_dsegment, V.dL_ddepth,
-                                       V.dL_dalpha, contrib, written, sv);
+                                       V.dL_dalpha, contrib, written, at<float>(im, IL.ckpt), sv);
             }
             if (int rc = check("render backward", sv, dbg)) return rc;
         } else {

@@ -197,8 +197,11 @@ inline size_t scratch_bytes(size_t I) { return align_up(I * 12 * sizeof(float)) 
 //                       steps of BQ_STEP list positions) and the backward walks the buckets
 //                       deepest first;
 //   tdone[T]:           split forward tiles: sum over finished halves of (depth << 1) | 1.
-// bq_cnt and tdone are zeroed by the tile-order kernels.
-constexpr int SCHED_FWD_SPLIT = 0, SCHED_FWD_QUARTER = 1, SCHED_WORDS = 4;
+// bq_cnt and tdone are zeroed by the tile-order kernels.  A queue entry is a tile index with a
+// list-segment kind in bits 30-31 (BQ_WHOLE / BQ_FRONT / BQ_BACK, render.hip): a tile replayed
+// deeper than the forward's checkpoint position sched[SCHED_CKPT] is filed as two entries, so a
+// bucket holds up to 2T entries.
+constexpr int SCHED_FWD_SPLIT = 0, SCHED_FWD_QUARTER = 1, SCHED_CKPT = 2, SCHED_WORDS = 4;
 constexpr int BQ_BUCKETS = 64, BQ_STEP = 16;
 struct TileSched {
     uint32_t *sched, *bq_cnt, *tdone, *bq_list;
@@ -211,14 +214,18 @@ __host__ __device__ inline TileSched tile_sched(uint32_t* order, int T) {
     s.bq_list = s.tdone + T;
     return s;
 }
-inline size_t tile_sched_words(size_t T) { return T + SCHED_WORDS + BQ_BUCKETS + T + BQ_BUCKETS * T; }
+__host__ __device__ inline size_t bq_cap(size_t T) { return 2 * T; }  // entries per bucket
+inline size_t tile_sched_words(size_t T) { return T + SCHED_WORDS + BQ_BUCKETS + T + BQ_BUCKETS * bq_cap(T); }
 // depth (1-based deepest contributor) -> backward bucket; 0 = nothing to replay
 __host__ __device__ inline uint32_t depth_bucket(uint32_t d) {
     const uint32_t b = (d + BQ_STEP - 1) / BQ_STEP;
     return b < (uint32_t)BQ_BUCKETS ? b : (uint32_t)BQ_BUCKETS - 1;
 }
+// Forward checkpoint of a tile (render.hip, list segments): 9 channels x 4 quadrants x 64 lanes
+// floats -- the backward's replay state at the checkpoint position (render.hip publish_depth).
+constexpr int CKPT_FLOATS = 9 * TILE_PIX;
 struct ImgLayout {
-    size_t ranges, n_contrib, order, bytes;
+    size_t ranges, n_contrib, order, ckpt, bytes;
     int gx, gy;
 };
 inline ImgLayout img_layout(int W, int H) {
@@ -231,6 +238,7 @@ inline ImgLayout img_layout(int W, int H) {
     L.ranges = take(T * 8);
     L.n_contrib = take(T * TILE_PIX * 4);  // tile-major: [tile][local pixel]
     L.order = take(tile_sched_words(T) * 4);  // heavy-first tile order + the render schedule (TileSched)
+    L.ckpt = take(T * CKPT_FLOATS * 4);       // forward checkpoints for the backward's list segments
     L.bytes = o + ALIGN;
     return L;
 }
@@ -361,12 +369,16 @@ void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, con
 void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
                            const uint2* ranges, const uint32_t* point_list, const float4* rec, const float* bg,
                            float* out_color, float* out_depth, float* out_alpha, float* out_segment,
-                           uint32_t* n_contrib, hipStream_t st);
+                           uint32_t* n_contrib, float* ckpt, hipStream_t st);
 void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
                             const uint2* ranges, const uint32_t* point_list, const uint32_t* slot_vals,
                             const float4* rec, const float* bg, const float* alpha, const uint32_t* n_contrib,
                             const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
-                            const float* dL_dalpha, float* contrib, uint8_t* written, hipStream_t st);
+                            const float* dL_dalpha, float* contrib, uint8_t* written, const float* ckpt,
+                            hipStream_t st);
+// list-segment checkpoint position of the render forward (0 = off; gsr_set_option "bwd_ckpt")
+void set_bwd_ckpt(int pos);
+int bwd_ckpt();
 
 uint32_t higher_msb(uint32_t n);
 

@@ -241,7 +241,31 @@ __device__ __forceinline__ bool tile_hit(float x, float y, float a, float b, flo
 // with it).  Lane 0 only.
 // Quarter tiles (4 parts): the word holds (max depth << 2) | parts done, updated by a
 // compare-and-swap loop; the part that completes the count files the tile.
-__device__ __forceinline__ void publish_depth(const TileSched& ts, int T, int tile, int parts, uint32_t d) {
+// List segments.  The backward replays a tile's list back to front, and its wave time grows with
+// the positions it replays; with one wave per tile the deepest tiles, four or five to a SIMD from
+// the start, set the kernel's end (profiles/round4_wave_trace.txt: per-SIMD work 1874..2407 list
+// positions, the kernel ends with the most loaded SIMD).  So the forward, when its list walk
+// reaches position ck (a multiple of 64, gsr_set_option "bwd_ckpt"), stores each pixel's
+// transmittance Tc and its seven channel sums (colour, segment, depth, weight) there, and at its
+// end turns them into the backward's replay state at ck (CKPT_FLOATS channels):
+//   [0]    T(ck) as the backward's chain has it: T_final * Tc / T_end, where T_final = 1 - weight
+//          sum is the reference's (backward.cu:468) and T_end the forward's last product -- the
+//          back's divisions would have reached T_final / prod_{j >= ck} (1 - alpha_j) with the same
+//          T_final rounding, which dominates for small T_final, and T_end / Tc is that product;
+//   [1..7] (sum_final - sum_at_ck) / Tc per channel: the normalised suffix sums of Dk (bwd_tile)
+//          for every channel (the reference's accum_rec, backward.cu:567-606);
+//   [8]    T_end / Tc: the product of (1 - alpha) over the suffix, which scales the background term
+// so Dk(ck) = sum_ch dL_ch [ch] + (bg . dL_dpix) [8].  A tile replayed deeper than ck + CK_MIN_BACK
+// is filed as two independent queue entries: the back [ck, d) starts at the end of the list as
+// before, the front [0, ck) from the checkpoint.  Every list position is replayed by exactly one
+// of them (records and written flags unchanged).
+constexpr uint32_t BQ_FRONT = 1u << 30, BQ_BACK = 2u << 30, BQ_TILE = BQ_FRONT - 1;
+constexpr uint32_t CK_MIN_BACK = 64;  // a back segment of at least one batch
+#ifndef GSR_BWD_CKPT
+#define GSR_BWD_CKPT 256
+#endif
+static int g_bwd_ckpt = GSR_BWD_CKPT;
+__device__ __forceinline__ void publish_depth(const TileSched& ts, int T, int tile, int parts, uint32_t d, int ck) {
     if (parts == 2) {
         const uint32_t old = atomicAdd(&ts.tdone[tile], (d << 1) | 1u);
         if (!(old & 1u)) return;  // first half: the second files the tile
@@ -256,10 +280,17 @@ __device__ __forceinline__ void publish_depth(const TileSched& ts, int T, int ti
         if ((old & 3u) != 3u) return;  // not the last quarter
         d = max(d, old >> 2);
     }
+    if (d == 0) return;  // nothing for the backward to replay
+    const size_t cap = bq_cap(T);
+    if (ck > 0 && d >= (uint32_t)ck + CK_MIN_BACK) {
+        // two list segments: the front [0, ck) from the forward's checkpoint, the back [ck, d)
+        const uint32_t bf = depth_bucket((uint32_t)ck), bb = depth_bucket(d - (uint32_t)ck);
+        ts.bq_list[(size_t)bf * cap + atomicAdd(&ts.bq_cnt[bf], 1u)] = (uint32_t)tile | BQ_FRONT;
+        ts.bq_list[(size_t)bb * cap + atomicAdd(&ts.bq_cnt[bb], 1u)] = (uint32_t)tile | BQ_BACK;
+        return;
+    }
     const uint32_t b = depth_bucket(d);
-    if (b == 0) return;  // nothing for the backward to replay
-    const uint32_t pos = atomicAdd(&ts.bq_cnt[b], 1u);
-    ts.bq_list[(size_t)b * T + pos] = (uint32_t)tile;
+    ts.bq_list[(size_t)b * cap + atomicAdd(&ts.bq_cnt[b], 1u)] = (uint32_t)tile;
 }
 
 template <int NQ>
@@ -268,7 +299,8 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
                                          const float4* __restrict__ rec, const float* __restrict__ bg,
                                          float* __restrict__ out_color, float* __restrict__ out_depth,
                                          float* __restrict__ out_alpha, float* __restrict__ out_segment,
-                                         uint32_t* __restrict__ n_contrib, float4 (*srec)[4]) {
+                                         uint32_t* __restrict__ n_contrib, float* __restrict__ ckpt, int ck,
+                                         float4 (*srec)[4]) {
     // The backward recovers T from T_final = 1 - sum(alpha*T) (backward.cu:468) and
     // divides back through every contributor, which amplifies a last-bit difference
     // in the weight sum by 1/T_final.  power, alpha, T and the weight sum are therefore
@@ -328,11 +360,30 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
     Batch cur;
     if (n > 0) cur = fetch_batch(rec, g_next);
     if (n > 0) g_next = plist[min(64 + lane, nlast)];
+    bool wrote_ck = false;
     for (int base = 0; base < n; base += 64) {
         uint64_t any_live = 0;
 #pragma unroll
         for (int kk = 0; kk < NQ; ++kk) any_live |= live[kk];
         if (!any_live) break;
+        if (ck > 0 && base == ck) {  // list-segment checkpoint (publish_depth): T and the sums so far
+            // wave-uniform base + 32-bit lane offsets (saddr stores: no per-lane 64-bit addresses
+            // for the compiler to keep live across the loop)
+            float* cp = ckpt + (size_t)__builtin_amdgcn_readfirstlane(tile) * CKPT_FLOATS;
+#pragma unroll
+            for (int kk = 0; kk < NQ; ++kk) {
+                const uint32_t o = 64u * (uint32_t)(q0 + kk) + (uint32_t)lane;
+                cp[o + 0 * TILE_PIX] = T[kk];
+                cp[o + 1 * TILE_PIX] = C0[kk];
+                cp[o + 2 * TILE_PIX] = C1[kk];
+                cp[o + 3 * TILE_PIX] = C2[kk];
+                cp[o + 4 * TILE_PIX] = S0[kk];
+                cp[o + 5 * TILE_PIX] = S1[kk];
+                cp[o + 6 * TILE_PIX] = Dp[kk];
+                cp[o + 7 * TILE_PIX] = Wt[kk];
+            }
+            wrote_ck = true;
+        }
         const int cnt = min(64, n - base);
         STAT(5, 1);
         const Batch nxt = fetch_batch(rec, g_next);
@@ -454,7 +505,25 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
     for (int kk = 0; kk < NQ; ++kk) deepest = max(deepest, last[kk]);
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) deepest = max(deepest, (uint32_t)__shfl_xor((int)deepest, o, 64));
-    if (lane == 0) publish_depth(ts, ntiles, tile, 4 / NQ, deepest);
+    if (lane == 0) publish_depth(ts, ntiles, tile, 4 / NQ, deepest, ck);
+    if (wrote_ck) {  // the checkpoint becomes the backward's replay state at ck (publish_depth)
+        float* cp = ckpt + (size_t)__builtin_amdgcn_readfirstlane(tile) * CKPT_FLOATS;
+#pragma unroll
+        for (int kk = 0; kk < NQ; ++kk) {
+            const uint32_t o = 64u * (uint32_t)(q0 + kk) + (uint32_t)lane;
+            const float Tc = cp[o];
+            const float rT = 1.0f / Tc;  // T(ck) > 0: at least T_MIN * 0.01 on any pixel
+            cp[o + 0 * TILE_PIX] = (1.0f - Wt[kk]) * (Tc / T[kk]);
+            cp[o + 1 * TILE_PIX] = (C0[kk] - cp[o + 1 * TILE_PIX]) * rT;
+            cp[o + 2 * TILE_PIX] = (C1[kk] - cp[o + 2 * TILE_PIX]) * rT;
+            cp[o + 3 * TILE_PIX] = (C2[kk] - cp[o + 3 * TILE_PIX]) * rT;
+            cp[o + 4 * TILE_PIX] = (S0[kk] - cp[o + 4 * TILE_PIX]) * rT;
+            cp[o + 5 * TILE_PIX] = (S1[kk] - cp[o + 5 * TILE_PIX]) * rT;
+            cp[o + 6 * TILE_PIX] = (Dp[kk] - cp[o + 6 * TILE_PIX]) * rT;
+            cp[o + 7 * TILE_PIX] = (Wt[kk] - cp[o + 7 * TILE_PIX]) * rT;
+            cp[o + 8 * TILE_PIX] = T[kk] * rT;
+        }
+    }
     WT_END(0, wslot, tile, n, deepest, NQ)
     const float bg0 = bg[0], bg1 = bg[1], bg2 = bg[2];
     const size_t HW = (size_t)H * W;
@@ -483,31 +552,32 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
 // 0.206 ms without; n >= 2048: 0.222, >= 1024: 0.233, >= 512: 0.246, >= 256: 0.241): each quarter
 // wave repeats the batch loads, the prefilter and the per-instance record reads and ballots for
 // one 8x8 quadrant (profiles/round3_quarter_sweep.txt).
-__global__ void __launch_bounds__(64) k_render_fwd(int W, int H, int gx, int T, const uint32_t* __restrict__ order,
+__global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(5))) k_render_fwd(int W, int H, int gx, int T, const uint32_t* __restrict__ order,
                                                    uint32_t* __restrict__ sched,
                                                    const uint2* __restrict__ ranges,
                                                    const uint32_t* __restrict__ point_list,
                                                    const float4* __restrict__ rec, const float* __restrict__ bg,
                                                    float* __restrict__ out_color, float* __restrict__ out_depth,
                                                    float* __restrict__ out_alpha, float* __restrict__ out_segment,
-                                                   uint32_t* __restrict__ n_contrib) {
+                                                   uint32_t* __restrict__ n_contrib, float* __restrict__ ckpt, int ck) {
     __shared__ float4 srec[64][4];
     const TileSched ts = tile_sched(sched - T, T);
+    if (blockIdx.x == 0 && threadIdx.x == 0) sched[SCHED_CKPT] = (uint32_t)ck;  // for the backward
     const uint32_t Hs = min(sched[SCHED_FWD_SPLIT], (uint32_t)T);
     const uint32_t Qs = min(sched[SCHED_FWD_QUARTER], Hs);
     const uint32_t b = blockIdx.x;
     if (b < 4 * Qs) {
         fwd_tile<1>(W, H, gx, T, (int)order[b >> 2], (int)(b & 3), (int)b, ts, ranges, point_list, rec, bg,
-                    out_color, out_depth, out_alpha, out_segment, n_contrib, srec);
+                    out_color, out_depth, out_alpha, out_segment, n_contrib, ckpt, ck, srec);
     } else if (b < 4 * Qs + 2 * (Hs - Qs)) {
         const uint32_t h = b - 4 * Qs;
         fwd_tile<2>(W, H, gx, T, (int)order[Qs + (h >> 1)], 2 * (int)(h & 1), (int)b, ts, ranges, point_list, rec,
-                    bg, out_color, out_depth, out_alpha, out_segment, n_contrib, srec);
+                    bg, out_color, out_depth, out_alpha, out_segment, n_contrib, ckpt, ck, srec);
     } else {
         const uint32_t i = b - 2 * Qs - Hs;  // = Hs + (b - 4 Qs - 2 (Hs - Qs))
         if (i >= (uint32_t)T) return;
         fwd_tile<4>(W, H, gx, T, (int)order[i], 0, (int)b, ts, ranges, point_list, rec, bg, out_color, out_depth,
-                    out_alpha, out_segment, n_contrib, srec);
+                    out_alpha, out_segment, n_contrib, ckpt, ck, srec);
     }
 }
 
@@ -609,7 +679,9 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                                          const float* __restrict__ dL_ddepths,
                                          const float* __restrict__ dL_dalphas,
                                          float* __restrict__ contrib, uint8_t* __restrict__ written,
-                                         float4 (*srec)[4], BwdShared* sh, float4 (*stage)[3] = nullptr) {
+                                         float4 (*srec)[4], BwdShared* sh, float4 (*stage)[3] = nullptr,
+                                         int seg_lo = 0, int seg_hi = 0x7fffffff,
+                                         const float* __restrict__ ckpt = nullptr) {
 #pragma clang fp contract(off)
     WT_BEGIN
     const int lane = threadIdx.x & 63, wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -662,11 +734,25 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
         bgd += bg1 * dp1[k];
         bgd += bg2 * dp2[k];
         Dk[k] = bgd;
+        if (ckpt != nullptr && lastc[k] > (uint32_t)seg_hi) {
+            // front segment (publish_depth): the replay state at seg_hi from the forward's checkpoint
+            const float* q = ckpt + (size_t)tile * CKPT_FLOATS + fidx;
+            float d = bgd * q[8 * TILE_PIX];
+            d = __builtin_fmaf(dp0[k], q[1 * TILE_PIX], d);
+            d = __builtin_fmaf(dp1[k], q[2 * TILE_PIX], d);
+            d = __builtin_fmaf(dp2[k], q[3 * TILE_PIX], d);
+            d = __builtin_fmaf(ds0[k], q[4 * TILE_PIX], d);
+            d = __builtin_fmaf(ds1[k], q[5 * TILE_PIX], d);
+            d = __builtin_fmaf(dd[k], q[6 * TILE_PIX], d);
+            d = __builtin_fmaf(da[k], q[7 * TILE_PIX], d);
+            Dk[k] = d;
+            T[k] = q[0];
+        }
         maxlast = max(maxlast, lastc[k]);
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) maxlast = max(maxlast, (uint32_t)__shfl_xor((int)maxlast, o, 64));
-    int top0 = (int)__builtin_amdgcn_readfirstlane(maxlast);
+    int top0 = min((int)__builtin_amdgcn_readfirstlane(maxlast), seg_hi);
     if constexpr (SPLIT) {  // both waves walk the same batches (their barriers pair up)
         if (lane == 0) sh->top[wid] = (uint32_t)top0;
         __syncthreads();
@@ -720,8 +806,8 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
         }
     };
     auto replay = [&]() {
-        for (int top = top0; top > 0; top -= 64) {
-            const int cnt = min(64, top);
+        for (int top = top0; top > seg_lo; top -= 64) {
+            const int cnt = min(64, top - seg_lo);
             STAT(5, 1);
             flush();
             const Batch nxt = fetch_batch(rec, g_next);
@@ -940,14 +1026,16 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
 // then two tiles per block, one per wave.  The grid is sized for no split (T / 2 ... T
 // blocks); blocks or waves past the queue return.  A tile's wave time grows with its
 // depth (the list positions it replays), so deepest-first is the longest-first order.
-__device__ __forceinline__ int queue_tile(const TileSched& ts, int T, uint32_t i, uint32_t pre, uint32_t cnt) {
+// Returns the queue entry (tile | segment kind, publish_depth), or BQ_NONE past the queue.
+constexpr uint32_t BQ_NONE = ~0u;
+__device__ __forceinline__ uint32_t queue_tile(const TileSched& ts, int T, uint32_t i, uint32_t pre, uint32_t cnt) {
     // pre / cnt: this lane's bucket (63 - lane) exclusive prefix and count (lane 63: bucket 0, empty)
     const uint64_t m = __builtin_amdgcn_ballot_w64(cnt > 0 && pre <= i);
-    if (!m) return -1;
+    if (!m) return BQ_NONE;
     const int L = 63 - __builtin_clzll(m);  // the last non-empty bucket starting at or before i
     const uint32_t pL = __builtin_amdgcn_readlane(pre, L), cL = __builtin_amdgcn_readlane(cnt, L);
-    if (i >= pL + cL) return -1;
-    return __builtin_amdgcn_readfirstlane((int)ts.bq_list[(size_t)(63 - L) * T + (i - pL)]);
+    if (i >= pL + cL) return BQ_NONE;
+    return (uint32_t)__builtin_amdgcn_readfirstlane((int)ts.bq_list[(size_t)(63 - L) * bq_cap(T) + (i - pL)]);
 }
 
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k_render_bwd(
@@ -974,8 +1062,11 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k
     const uint32_t Hs = sb < 64 ? (uint32_t)__builtin_amdgcn_readlane(pre + cnt, 63 - sb) : 0u;
     const uint32_t b = blockIdx.x;
     const bool split = b < Hs;  // block-uniform
-    const int tile = queue_tile(ts, T, split ? b : Hs + 2 * (b - Hs) + (uint32_t)wid, pre, cnt);
-    if (tile < 0) return;  // past the queue (a split block's waves share the tile: both return or neither)
+    const uint32_t e = queue_tile(ts, T, split ? b : Hs + 2 * (b - Hs) + (uint32_t)wid, pre, cnt);
+    if (e == BQ_NONE) return;  // past the queue (a split block's waves share the tile: both return or neither)
+    // the forward runs without list segments for this kernel (launch_render_forward); a segment
+    // entry would be replayed whole, i.e. its records written twice with the same values
+    const int tile = (int)(e & BQ_TILE);
     if (split) {
         bwd_tile<2, true>(W, H, gx, tile, 2 * wid, (int)(2 * b + wid), ranges, point_list, slot_vals, rec, bg,
                           alphas, n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written,
@@ -1000,7 +1091,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD
     const float4* __restrict__ rec, const float* __restrict__ bg, const float* __restrict__ alphas,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ dL_dsegs,
     const float* __restrict__ dL_ddepths, const float* __restrict__ dL_dalphas, float* __restrict__ contrib,
-    uint8_t* __restrict__ written) {
+    uint8_t* __restrict__ written, const float* __restrict__ ckpt) {
     __shared__ float4 srec[64][4];
     __shared__ float4 stage[64][3];
     const int lane = threadIdx.x & 63;
@@ -1013,38 +1104,50 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD
         if (lane >= o) pre += y;
     }
     pre -= cnt;
-    const int tile = queue_tile(ts, T, blockIdx.x, pre, cnt);
-    if (tile < 0) return;
-    bwd_tile<4, false>(W, H, gx, tile, 0, (int)blockIdx.x, ranges, point_list, slot_vals, rec, bg, alphas, n_contrib,
-                       dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, srec, nullptr, stage);
+    const uint32_t e = queue_tile(ts, T, blockIdx.x, pre, cnt);
+    if (e == BQ_NONE) return;
+    // a whole tile, or one of its list segments [0, ck) / [ck, depth) (publish_depth)
+    const uint32_t kind = e & ~BQ_TILE;
+    const int ck = (int)ts.sched[SCHED_CKPT];
+    bwd_tile<4, false>(W, H, gx, (int)(e & BQ_TILE), 0, (int)blockIdx.x, ranges, point_list, slot_vals, rec,
+                       bg, alphas, n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, srec,
+                       nullptr, stage, kind == BQ_BACK ? ck : 0, kind == BQ_FRONT ? ck : 0x7fffffff,
+                       kind == BQ_FRONT ? ckpt : nullptr);
 }
 
 }  // namespace
 
+void set_bwd_ckpt(int pos) { g_bwd_ckpt = pos > 0 ? (pos + 63) / 64 * 64 : 0; }
+int bwd_ckpt() { return g_bwd_ckpt; }
+
 void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
                            const uint2* ranges, const uint32_t* point_list, const float4* rec, const float* bg,
                            float* out_color, float* out_depth, float* out_alpha, float* out_segment,
-                           uint32_t* n_contrib, hipStream_t st) {
+                           uint32_t* n_contrib, float* ckpt, hipStream_t st) {
     const int T = gx * gy;
     if (T == 0) return;
+    // list segments only for the one-wave backward (k_render_bwd1)
+    const int ck = split_bwd_depth() <= 0 ? g_bwd_ckpt : 0;
     // grid for the worst case of the schedule: 2T blocks with halves only, 4T with quarters
     hipLaunchKernelGGL(k_render_fwd, dim3((split4_fwd_bucket() > 0 ? 4 : 2) * T), dim3(64), 0, st, W, H, gx, T, order,
                        sched, ranges, point_list,
-                       rec, bg, out_color, out_depth, out_alpha, out_segment, n_contrib);
+                       rec, bg, out_color, out_depth, out_alpha, out_segment, n_contrib, ckpt, ck);
 }
 
 void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
                             const uint2* ranges, const uint32_t* point_list, const uint32_t* slot_vals,
                             const float4* rec, const float* bg, const float* alpha, const uint32_t* n_contrib,
                             const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
-                            const float* dL_dalpha, float* contrib, uint8_t* written, hipStream_t st) {
+                            const float* dL_dalpha, float* contrib, uint8_t* written, const float* ckpt,
+                            hipStream_t st) {
     const int T = gx * gy;
     if (T == 0) return;
     (void)order;  // the backward follows the forward's depth queue
     if (split_bwd_depth() <= 0) {
-        hipLaunchKernelGGL(k_render_bwd1, dim3(T), dim3(64), 0, st, W, H, gx, T, sched, ranges, point_list,
+        // up to two queue entries per tile (list segments); blocks past the queue return at once
+        hipLaunchKernelGGL(k_render_bwd1, dim3(2 * T), dim3(64), 0, st, W, H, gx, T, sched, ranges, point_list,
                            slot_vals, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha,
-                           contrib, written);
+                           contrib, written, ckpt);
         return;
     }
     hipLaunchKernelGGL(k_render_bwd, dim3(T), dim3(128), 0, st, W, H, gx, T, split_bwd_depth(), sched, ranges,

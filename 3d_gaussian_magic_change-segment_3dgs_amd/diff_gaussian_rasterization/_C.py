@@ -142,7 +142,7 @@ def debug_state(name, P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffe
     gsr_debug_copy in include/gsr.h).  Unsigned arrays are returned as int32."""
     dtype, per, unit = _DEBUG_FIELDS[name]
     T = ((W + 15) // 16) * ((H + 15) // 16)
-    n = {"P": P, "I": num_rendered, "T": T, "T+": T + 4 + 64 + T + 64 * T}[unit] * per
+    n = {"P": P, "I": num_rendered, "T": T, "T+": T + 4 + 64 + T + 64 * 2 * T}[unit] * per
     dev = geomBuffer.device
     out = torch.empty(max(n, 1), dtype=dtype, device=dev)
     ptr = lambda t: t.data_ptr() if t is not None and t.numel() else None

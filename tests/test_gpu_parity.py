@@ -334,12 +334,38 @@ def test_rows_binning_matches_radix_path(gpu_available, case):
 
 
 def _tile_queue(state, T):
-    """The render schedule after the T-entry tile order (gsr_internal.h TileSched)."""
-    t = state["tile_order"].astype(np.int64)
+    """The render schedule after the T-entry tile order (gsr_internal.h TileSched): sched words,
+    bucket counts, bucket lists (2T entries each: tile | kind << 30; the debug copy is int32, so
+    it is read as uint32)."""
+    t = np.ascontiguousarray(state["tile_order"]).view(np.uint32).astype(np.int64)
     sched = t[T:T + 4]
     cnt = t[T + 4:T + 68]
-    lst = t[T + 68 + T:].reshape(64, T)
+    lst = t[T + 68 + T:].reshape(64, 2 * T)
     return sched, cnt, lst
+
+
+def _check_queue(state, T):
+    """Every tile with a contributor is filed once under ceil(depth / 16) (capped at 63), or,
+    deeper than the checkpoint position ck + 64 (sched[SCHED_CKPT]), as a front segment [0, ck)
+    under ck's bucket and a back segment [ck, depth) under its own (render.hip publish_depth).
+    Returns (ck, number of split tiles)."""
+    sched, cnt, lst = _tile_queue(state, T)
+    ck = int(sched[2])
+    depth = state["n_contrib_tiles"].reshape(T, 256).max(1).astype(np.int64)
+    bk = lambda d: np.minimum((d + 15) // 16, 63)  # noqa: E731
+    assert cnt[0] == 0
+    ent = np.concatenate([lst[k, :cnt[k]] for k in range(64)])
+    bucket_of = np.concatenate([np.full(int(cnt[k]), k) for k in range(64)])
+    tile, kind = ent & ((1 << 30) - 1), ent >> 30
+    split = (depth >= ck + 64) if ck > 0 else np.zeros(T, bool)
+    want = {(int(t), 0) for t in np.nonzero((depth > 0) & ~split)[0]}
+    want |= {(int(t), k) for t in np.nonzero(split)[0] for k in (1, 2)}
+    got = list(zip(tile.tolist(), kind.tolist()))
+    assert len(got) == len(set(got)) and set(got) == want, "queue entries"
+    for (t, k), b in zip(got, bucket_of.tolist()):
+        d = depth[t] if k == 0 else ck if k == 1 else depth[t] - ck
+        assert b == bk(d), f"tile {t} kind {k} in bucket {b}"
+    return ck, int(split.sum())
 
 
 @pytest.mark.parametrize("split,rows", [((1, 1), 1), ((1, 0), 1), ((0, 1), 1), ((1, 1), 0), ((10, 256), 1),
@@ -381,13 +407,8 @@ def test_split_tiles(gpu_available, oracle_mod, split, rows):
     if len(split) > 2:
         assert sched[1] == int((lens >= (1 << (split[2] - 1))).sum()) > 0, "forward quarter count"
     assert _tile_queue(b, T)[0][0] == 0
-    # the queue: every tile with a contributor once, under ceil(depth / 16) (capped at 63)
-    depth = a["n_contrib_tiles"].reshape(T, 256).max(1).astype(np.int64)
-    bucket = np.minimum((depth + 15) // 16, 63)
-    filed = np.concatenate([lst[k, :cnt[k]] for k in range(64)])
-    assert cnt[0] == 0 and len(filed) == int((depth > 0).sum()) == len(set(filed.tolist()))
-    for k in range(1, 64):
-        assert np.all(bucket[lst[k, :cnt[k]]] == k), f"bucket {k}"
+    ck, _ = _check_queue(a, T)
+    assert (ck == 0) == (split[1] > 0), "list segments only with the one-wave backward"
     for k in ("n_contrib", "color", "depth", "alpha", "segment", "radii"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     r = Hn.run_oracle(oracle_mod, scene, cam, grads=grads)
@@ -397,3 +418,43 @@ def test_split_tiles(gpu_available, oracle_mod, split, rows):
     if split[1] == 0:  # backward unsplit: gradients bit-identical
         for k in a["grads"]:
             np.testing.assert_array_equal(a["grads"][k], b["grads"][k], err_msg=k)
+
+
+@pytest.mark.parametrize("ck,rows", [(64, 1), (128, 1), (192, 0), (0, 1)])
+def test_list_segments(gpu_available, oracle_mod, ck, rows):
+    """Backward list segments (render.hip publish_depth): the forward checkpoints every pixel's
+    T and channel remainders at list position ck, and tiles replayed deeper than ck + 64 are
+    queued as a front [0, ck) and a back [ck, depth) segment on separate waves.  Forced low on a
+    small scene so most tiles split.  Checked: the queue (each tile's segments once, in the
+    right buckets), forward outputs bit-identical to the unsegmented run, gradients within the
+    parity tolerance of the oracle and within 1e-5 of the unsegmented run's (the front's state
+    comes from the forward's products instead of the back's divisions)."""
+    from diff_gaussian_rasterization import _C
+    scene, cam = synthetic_scene(60000, sh_degree=3, seed=41), orbit_camera(2, 640, 360, 400.0)
+    grads = Hn.upstream_grads(cam.height, cam.width)
+    out = {}
+    try:
+        _C.set_option("rows_binning", rows)
+        for mode in (ck, 0):
+            _C.set_option("bwd_ckpt", mode)
+            out[mode] = Hn.run_gsr(scene, cam, grads=grads)
+    finally:
+        _C.set_option("rows_binning", 1)
+        _C.set_option("bwd_ckpt", 256)
+    a, b = out[ck], out[0]
+    T = ((cam.width + 15) // 16) * ((cam.height + 15) // 16)
+    got_ck, nsplit = _check_queue(a, T)
+    assert got_ck == ck
+    if ck:
+        assert nsplit > T // 4, f"only {nsplit} of {T} tiles split at ck={ck}"
+    assert _check_queue(b, T) == (0, 0)
+    for k in ("n_contrib", "color", "depth", "alpha", "segment", "radii"):
+        np.testing.assert_array_equal(a[k], b[k], err_msg=k)
+    r = Hn.run_oracle(oracle_mod, scene, cam, grads=grads)
+    r.pop("_run", None)
+    assert_grad_parity(a["grads"], r["grads"])
+    for k in a["grads"]:
+        ref = b["grads"][k]
+        tol = 1e-5 * max(float(np.abs(ref).max()), 1e-30)
+        err = float(np.abs(a["grads"][k] - ref).max()) if ref.size else 0.0
+        assert err <= tol, f"{k}: segmented vs whole max |diff| {err:.3g} > {tol:.3g}"

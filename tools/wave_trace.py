@@ -88,7 +88,7 @@ def main():
     slots = props.multi_processor_count * 4 * 4  # 4 SIMDs per CU x 4 waves per SIMD (the kernels' cap)
     res = {}
     for k, name in enumerate(("k_render_fwd", "k_render_bwd")):
-        r = analyse(name, buf[k], slots if k == 1 else props.multi_processor_count * 4 * int(os.environ.get("GSR_FWD_WAVES", "5")))
+        r = analyse(name, buf[k], props.multi_processor_count * 4 * int(os.environ.get("GSR_BWD_WAVES", "5")) if k == 1 else props.multi_processor_count * 4 * int(os.environ.get("GSR_FWD_WAVES", "5")))
         res.update({f"{name}_{a}": v for a, v in r.items()})
     if out:
         np.savez_compressed(out, **res)
