@@ -46,26 +46,30 @@
 // T_final = 1 - sum(alpha*T) (backward.cu:468), amplifying any last-ulp alpha
 // difference by 1/T_final.  gsr therefore evaluates exp() with gsr_expf below:
 // IEEE operations only (fma, add, mul, integer shift), so the CPU oracle computes the
-// very same bits (oracle/gsr_oracle.cpp: gsr_expf).  Max error 0.88 ulp,
-// correctly rounded on 99.53% of inputs (tests/test_oracle_golden.py pins it
-// against double-precision exp; the reference's CUDA expf is specified at 2 ulp).
+// very same bits (oracle/gsr_oracle.cpp: gsr_expf).  On the blend's range [-5.6, 0] (powers at
+// or above the opacity floor, power_floor) max error 0.887 ulp, correctly rounded on 99.64% of
+// inputs (exhaustive; tests/test_oracle_golden.py pins it against double-precision exp; the
+// reference's CUDA expf is specified at 2 ulp).
 // GSR_FAST_EXP selects __expf (v_exp_f32, several ulp) for experiments.
 // power, alpha, T and the weight sum run without FMA contraction (see the
 // kernels); only non-amplified sums use explicit FMAs.
+// ln 2 rounded to fp32: the reduction x - k ln2 is one FMA.  Its error, |k| * 1.9e-9, is at most
+// 1.5e-8 on the blend's range (|k| <= 8) and grows to 2.4e-7 (< 5 ulp) at -87 and 88, where only rejected
+// pairs land (alpha < 1/255 with the power floor's 1e-3 margin).  The two-step Cody-Waite form it
+// replaced (hi + lo, one more FMA per exp): max 0.874 ulp, correctly rounded 99.71% on [-5.6, 0].
+constexpr float GSR_LN2 = 0.693147182464599609375f;
 __device__ __forceinline__ float gsr_expf(float x) {
     // exp(clamp(x, -87, 88)).  k = round(x log2 e) via the 1.5*2^23 shifter (one FMA,
-    // the integer lands in the low mantissa bits), Cody-Waite ln2 = hi + lo, degree-6
+    // the integer lands in the low mantissa bits), r = x - k ln2 (one FMA), degree-6
     // minimax polynomial on [-ln2/2, ln2/2] (1 + r + c2 r^2 + ... + c6 r^6, fp32
     // coefficients, Horner with FMAs), then times 2^k assembled from the shifter's
     // bits (k in [-126, 127], so the product is an exact scaling).  Outside the clamp
     // the value is meaningless for blending anyway: alpha < 1/255 below -87 and the
-    // blend rejects power > 0.  Exhaustive check over every fp32 in [-87, 0]: max 0.88
-    // ulp, correctly rounded on 99.53% (the degree-7 Taylor form it replaced: 0.94 ulp).
+    // blend rejects power > 0.
     const float xc = __builtin_amdgcn_fmed3f(x, -87.0f, 88.0f);
     const float kf = __builtin_fmaf(xc, 1.44269502f, 12582912.0f);
     const float k = kf - 12582912.0f;
-    float r = __builtin_fmaf(-k, 0.693145751953125f, xc);
-    r = __builtin_fmaf(-k, 1.42860677e-06f, r);
+    const float r = __builtin_fmaf(-k, GSR_LN2, xc);
     float p = 0.001381461275741458f;
     p = __builtin_fmaf(p, r, 0.008368710055947304f);
     p = __builtin_fmaf(p, r, 0.04166838899254799f);
@@ -86,8 +90,7 @@ __device__ __forceinline__ float gsr_expf(float x) {
 __device__ __forceinline__ float gsr_expf_nc(float x) {
     const float kf = __builtin_fmaf(x, 1.44269502f, 12582912.0f);
     const float k = kf - 12582912.0f;
-    float r = __builtin_fmaf(-k, 0.693145751953125f, x);
-    r = __builtin_fmaf(-k, 1.42860677e-06f, r);
+    const float r = __builtin_fmaf(-k, GSR_LN2, x);
     float p = 0.001381461275741458f;
     p = __builtin_fmaf(p, r, 0.008368710055947304f);
     p = __builtin_fmaf(p, r, 0.04166838899254799f);
@@ -252,8 +255,13 @@ __device__ __forceinline__ bool tile_hit(float x, float y, float a, float b, flo
 //          sum is the reference's (backward.cu:468) and T_end the forward's last product -- the
 //          back's divisions would have reached T_final / prod_{j >= ck} (1 - alpha_j) with the same
 //          T_final rounding, which dominates for small T_final, and T_end / Tc is that product;
-//   [1..7] (sum_final - sum_at_ck) / Tc per channel: the normalised suffix sums of Dk (bwd_tile)
-//          for every channel (the reference's accum_rec, backward.cu:567-606);
+//   [1..7] the channel sums from ck on, / Tc: the normalised suffix sums of Dk (bwd_tile) for every
+//          channel (the reference's accum_rec, backward.cu:567-606).  The colour, segment and depth
+//          sums restart from 0 at ck, so these are accumulated directly (as differences of prefix
+//          sums they lost eps * sum_final / Tc to cancellation, which the replay amplifies by
+//          1 / (1 - alpha) per front contributor: one C3 dscales element went from 4e-6 to 1.2e-5
+//          of its maximum); the weight sum from ck on is T(ck) - T_end (telescoping), since the
+//          weight sum itself must not restart (T_final = 1 - weight sum);
 //   [8]    T_end / Tc: the product of (1 - alpha) over the suffix, which scales the background term
 // so Dk(ck) = sum_ch dL_ch [ch] + (bg . dL_dpix) [8].  A tile replayed deeper than ck + CK_MIN_BACK
 // is filed as two independent queue entries: the back [ck, d) starts at the end of the list as
@@ -366,9 +374,12 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
 #pragma unroll
         for (int kk = 0; kk < NQ; ++kk) any_live |= live[kk];
         if (!any_live) break;
-        if (ck > 0 && base == ck) {  // list-segment checkpoint (publish_depth): T and the sums so far
-            // wave-uniform base + 32-bit lane offsets (saddr stores: no per-lane 64-bit addresses
-            // for the compiler to keep live across the loop)
+        if (ck > 0 && base == ck) {  // list-segment checkpoint (publish_depth)
+            // T and the colour / segment / depth sums so far, which then restart from 0: at the end
+            // they hold the sums from ck on (no cancellation, publish_depth) and the outputs are the
+            // two parts added (the weight sum runs on: T_final = 1 - weight sum must stay the
+            // reference's).  Wave-uniform base + 32-bit lane offsets (saddr stores: no per-lane
+            // 64-bit addresses for the compiler to keep live across the loop).
             float* cp = ckpt + (size_t)__builtin_amdgcn_readfirstlane(tile) * CKPT_FLOATS;
 #pragma unroll
             for (int kk = 0; kk < NQ; ++kk) {
@@ -380,7 +391,7 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
                 cp[o + 4 * TILE_PIX] = S0[kk];
                 cp[o + 5 * TILE_PIX] = S1[kk];
                 cp[o + 6 * TILE_PIX] = Dp[kk];
-                cp[o + 7 * TILE_PIX] = Wt[kk];
+                C0[kk] = C1[kk] = C2[kk] = S0[kk] = S1[kk] = Dp[kk] = 0.f;
             }
             wrote_ck = true;
         }
@@ -513,15 +524,23 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
             const uint32_t o = 64u * (uint32_t)(q0 + kk) + (uint32_t)lane;
             const float Tc = cp[o];
             const float rT = 1.0f / Tc;  // T(ck) > 0: at least T_MIN * 0.01 on any pixel
+            const float b0 = cp[o + 1 * TILE_PIX], b1 = cp[o + 2 * TILE_PIX], b2 = cp[o + 3 * TILE_PIX];
+            const float b3 = cp[o + 4 * TILE_PIX], b4 = cp[o + 5 * TILE_PIX], b5 = cp[o + 6 * TILE_PIX];
             cp[o + 0 * TILE_PIX] = (1.0f - Wt[kk]) * (Tc / T[kk]);
-            cp[o + 1 * TILE_PIX] = (C0[kk] - cp[o + 1 * TILE_PIX]) * rT;
-            cp[o + 2 * TILE_PIX] = (C1[kk] - cp[o + 2 * TILE_PIX]) * rT;
-            cp[o + 3 * TILE_PIX] = (C2[kk] - cp[o + 3 * TILE_PIX]) * rT;
-            cp[o + 4 * TILE_PIX] = (S0[kk] - cp[o + 4 * TILE_PIX]) * rT;
-            cp[o + 5 * TILE_PIX] = (S1[kk] - cp[o + 5 * TILE_PIX]) * rT;
-            cp[o + 6 * TILE_PIX] = (Dp[kk] - cp[o + 6 * TILE_PIX]) * rT;
-            cp[o + 7 * TILE_PIX] = (Wt[kk] - cp[o + 7 * TILE_PIX]) * rT;
+            cp[o + 1 * TILE_PIX] = C0[kk] * rT;
+            cp[o + 2 * TILE_PIX] = C1[kk] * rT;
+            cp[o + 3 * TILE_PIX] = C2[kk] * rT;
+            cp[o + 4 * TILE_PIX] = S0[kk] * rT;
+            cp[o + 5 * TILE_PIX] = S1[kk] * rT;
+            cp[o + 6 * TILE_PIX] = Dp[kk] * rT;
+            cp[o + 7 * TILE_PIX] = (Tc - T[kk]) * rT;  // weights from ck on: T(ck) - T_end (telescoping)
             cp[o + 8 * TILE_PIX] = T[kk] * rT;
+            C0[kk] = b0 + C0[kk];  // the outputs: the sums before ck plus those from ck on
+            C1[kk] = b1 + C1[kk];
+            C2[kk] = b2 + C2[kk];
+            S0[kk] = b3 + S0[kk];
+            S1[kk] = b4 + S1[kk];
+            Dp[kk] = b5 + Dp[kk];
         }
     }
     WT_END(0, wslot, tile, n, deepest, NQ)
@@ -641,7 +660,15 @@ __device__ __forceinline__ float fdiv(float num, float den) {
     const float r = __builtin_amdgcn_rcpf(den);
     const float q = num * r;
     const float e = __builtin_fmaf(-q, den, num);
+#ifndef GSR_DIV_NO_ASM
+    // the correction as a three-address v_fma_f32: as v_fmac (destination = q's register) the
+    // replay's loop-carried T needed a v_mov per strip to get back into its own register
+    float t;
+    asm("v_fma_f32 %0, %1, %2, %3" : "=v"(t) : "v"(e), "v"(r), "v"(q));
+    return t;
+#else
     return __builtin_fmaf(e, r, q);
+#endif
 #endif
 }
 

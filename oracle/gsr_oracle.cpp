@@ -262,19 +262,20 @@ static std::string g_err;
 
 // exp() of the blend (forward.cu:351, backward.cu:547).  The reference calls CUDA's
 // expf (2 ulp); gsr's kernels and this oracle share gsr_expf: IEEE operations only
-// (fma, add, mul, integer shift), max 0.88 ulp, so both compute identical bits and the
-// knife-edge blend decisions (alpha >= 1/255, T(1-alpha) >= 1e-4) agree exactly.
+// (fma, add, mul, integer shift), max 0.887 ulp on the blend's range [-5.6, 0], so both compute
+// identical bits and the knife-edge blend decisions (alpha >= 1/255, T(1-alpha) >= 1e-4) agree
+// exactly.
 // g_exp_libm = 1 switches to the C library's expf (noise-floor studies).
 static int g_exp_libm = 0;
 static inline float gsr_expf(float x) {
-    // exp(clamp(x, -87, 88)): k = round(x log2 e) by the 1.5*2^23 shifter, Cody-Waite
-    // reduction, degree-6 minimax polynomial (Horner, FMA), times 2^k built from the
-    // shifter's low bits.  Must stay bit-identical to render.hip: gsr_expf.
+    // exp(clamp(x, -87, 88)): k = round(x log2 e) by the 1.5*2^23 shifter, r = x - k ln2 with
+    // ln 2 rounded to fp32 (one FMA; error |k| * 1.9e-9), degree-6 minimax polynomial (Horner,
+    // FMA), times 2^k built from the shifter's low bits.  Must stay bit-identical to
+    // render.hip: gsr_expf.
     const float xc = std::fmin(std::fmax(x, -87.0f), 88.0f);
     const float kf = std::fma(xc, 1.44269502f, 12582912.0f);
     const float k = kf - 12582912.0f;
-    float r = std::fma(-k, 0.693145751953125f, xc);
-    r = std::fma(-k, 1.42860677e-06f, r);
+    const float r = std::fma(-k, 0.693147182464599609375f, xc);
     float p = 0.001381461275741458f;  // degree-6 minimax (1 + r + c2 r^2 + ... + c6 r^6)
     p = std::fma(p, r, 0.008368710055947304f);
     p = std::fma(p, r, 0.04166838899254799f);
