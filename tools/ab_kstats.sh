@@ -15,7 +15,7 @@ for r in $(seq 1 $R); do
     if [ -n "$so" ]; then export GSR_LIBRARY=$PWD/$so; else unset GSR_LIBRARY; fi
     d=gpurun_out/abk/${name}_$r
     rm -rf $d
-    timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $d -o kt --output-format csv -- python3 bench.py --steps 50 --warmup 5 \
+    timeout -k 10 240 rocprofv3 --kernel-trace --stats -d $d -o kt --output-format csv -- python3 bench.py --config ${CONFIG:-mt} --steps ${AB_STEPS:-50} --warmup 5 \
       --no-cpu-baseline --no-train --batched-views 1 > $d.log 2>&1 || { echo "$name failed"; tail -5 $d.log; exit 1; }
     f=$(find $d -name "*kernel_stats.csv" | head -1)
     echo "== $name r$r $(python tools/kstats.py $f | awk -v K="$K" 'BEGIN{split(K,a," ");for(i in a)w[a[i]]=1} {split($1,b,"<"); if (b[1] in w) printf "%s=%s ", b[1], $5}')"
