@@ -292,8 +292,14 @@ GSR_API const char* gsr_version(void);
  * "rows_binning" (0/1, default 1), "speculate" (0/1, default 1), "split_fwd_bucket" /
  * "split4_fwd_bucket" (forward tiles with n >= 2^(B-1) instances on two / four waves; defaults
  * 8 / 0 = off), "split_bwd_depth" (backward two-wave tiles; default 0 = off); a negative value
- * restores a default.  Results are identical either way.  Returns 0, or non-zero for an unknown
- * name. */
+ * restores a default.  Results are identical either way.  "bwd_ckpt" (list position, rounded up
+ * to a multiple of 64; default 256, 0 = off): the forward checkpoints each pixel's replay state
+ * there and the backward replays tiles deeper than it + 64 as two independent list segments
+ * (render.hip publish_depth); gradients then differ from the unsegmented ones in fp32 rounding
+ * (within the parity bounds) and colour / depth / segment outputs by a few ulps; it applies only
+ * with split_bwd_depth = 0 and is read by the forward (the backward follows the forward's choice).
+ * "mv_streams" (0/1, default 1): the multi-view backward's odd views on a second stream.
+ * Returns 0, or non-zero for an unknown name. */
 GSR_API int gsr_set_option(const char* name, long long value);
 
 #ifdef __cplusplus
