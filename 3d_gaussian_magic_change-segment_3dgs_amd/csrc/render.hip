@@ -268,7 +268,10 @@ __device__ __forceinline__ bool tile_hit(float x, float y, float a, float b, flo
 // before, the front [0, ck) from the checkpoint.  Every list position is replayed by exactly one
 // of them (records and written flags unchanged).
 constexpr uint32_t BQ_FRONT = 1u << 30, BQ_BACK = 2u << 30, BQ_TILE = BQ_FRONT - 1;
-constexpr uint32_t CK_MIN_BACK = 64;  // a back segment of at least one batch
+#ifndef GSR_CK_MIN_BACK
+#define GSR_CK_MIN_BACK 64
+#endif
+constexpr uint32_t CK_MIN_BACK = GSR_CK_MIN_BACK;  // a back segment of at least one batch
 #ifndef GSR_BWD_CKPT
 #define GSR_BWD_CKPT 256
 #endif

@@ -120,13 +120,35 @@ _lib.gsr_timing_collect.argtypes = [ctypes.POINTER(ctypes.c_double), ctypes.POIN
 _lib.gsr_stream_copy.restype = _i
 _lib.gsr_stream_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, _i, ctypes.c_void_p]
 
+# native data-parallel exchange (include/gsr.h, csrc/dp.hip): optional so that an older build
+# without it still imports (gsr_tools.dp then keeps the torch.distributed path)
+if hasattr(_lib, "gsr_dp_init"):
+    _lib.gsr_dp_unique_id_bytes.restype = _sz
+    _lib.gsr_dp_unique_id_bytes.argtypes = []
+    _lib.gsr_dp_get_unique_id.restype = _i
+    _lib.gsr_dp_get_unique_id.argtypes = [_vp]
+    _lib.gsr_dp_init.restype = _i
+    _lib.gsr_dp_init.argtypes = [_vp, _i, _i]
+    _lib.gsr_dp_world.restype = _i
+    _lib.gsr_dp_world.argtypes = []
+    _lib.gsr_dp_finalize.restype = _i
+    _lib.gsr_dp_finalize.argtypes = []
+    _lib.gsr_dp_allreduce.restype = _i
+    _lib.gsr_dp_allreduce.argtypes = [_vp, _sz, _vp]
+    _lib.gsr_dp_sh_exchange.restype = _i
+    _lib.gsr_dp_sh_exchange.argtypes = [_i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp]
+    _lib.gsr_dp_wait.restype = _i
+    _lib.gsr_dp_wait.argtypes = [_i, _vp]
+
 EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_binning_capacity", "gsr_img_bytes", "gsr_backward_scratch_bytes",
                     "gsr_forward_geometry", "gsr_forward_render", "gsr_forward", "gsr_backward", "gsr_mark_visible",
                     "gsr_debug_copy", "gsr_num_stages", "gsr_stage_name", "gsr_timing_enable", "gsr_timing_collect",
                     "gsr_stream_copy",
                     "gsr_last_error", "gsr_version", "gsr_set_option", "gsr_multiview_scratch_bytes",
                     "gsr_backward_multiview", "gsr_sh_rows_floats", "gsr_backward_multiview_deferred_sh",
-                    "gsr_sh_backward", "gsr_backward_deferred_sh")
+                    "gsr_sh_backward", "gsr_backward_deferred_sh", "gsr_dp_unique_id_bytes", "gsr_dp_get_unique_id",
+                    "gsr_dp_init", "gsr_dp_world", "gsr_dp_finalize", "gsr_dp_allreduce", "gsr_dp_sh_exchange",
+                    "gsr_dp_wait")
 
 _DEBUG_FIELDS = {  # name -> (dtype, elements per unit, unit: P | I | T)
     "tiles_touched": (torch.int32, 1, "P"), "rec": (torch.float32, 16, "P"), "clamped": (torch.uint8, 1, "P"),

@@ -17,6 +17,7 @@ Two exchanges give the same summed bucket:
     ShExchange 2(N-1)/N*52 + (N-1)*B*12 B -- 3.8x less at N=2, 2.4x at N=8 (B=1).
     choose_exchange() picks the cheaper one.
 """
+import ctypes
 import os
 import time
 
@@ -171,6 +172,93 @@ def measure_rebuild_us(P, M, views, device, degree=3, reps=5):
     return ts[len(ts) // 2]
 
 
+# ---- native exchange (csrc/dp.hip, include/gsr.h gsr_dp_*): the same collectives issued from C
+# over the library's own RCCL communicator.  torch.distributed's call path costs 25-35 us of host
+# time per collective; at one view per rank the SH exchange's start then took 130-170 us of a
+# 0.9-ms step and the host bounded the step (profiles/round4_c_rccl_world1_sh.json).
+_UNSET = object()
+_NATIVE = {"group": _UNSET}  # the group init_native set the native path up for
+
+
+def _lib():
+    from diff_gaussian_rasterization import _C
+    return _C
+
+
+def init_native(group=None):
+    """Set up the native RCCL exchange beside torch.distributed's group `group` (the default group
+    when None): group rank 0's unique id is broadcast over the group, every rank joins.  Collective:
+    every rank of the group calls it.  Returns True when the native path is active; False (the
+    torch.distributed path stays) with GSR_NATIVE_DP=0, a non-nccl backend or a library without
+    it."""
+    C = _lib()
+    L = C._lib
+    if (os.environ.get("GSR_NATIVE_DP", "1") == "0" or not hasattr(L, "gsr_dp_init")
+            or dist.get_backend(group) != "nccl"):
+        return False
+    if L.gsr_dp_world() > 0:
+        return _NATIVE["group"] is group
+    n = int(L.gsr_dp_unique_id_bytes())
+    uid = ctypes.create_string_buffer(n)
+    if dist.get_rank(group) == 0:
+        C._check(L.gsr_dp_get_unique_id(uid))
+    obj = [uid.raw]
+    dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    uid = ctypes.create_string_buffer(obj[0], n)
+    C._check(L.gsr_dp_init(uid, dist.get_world_size(group), dist.get_rank(group)))
+    _NATIVE["group"] = group
+    return True
+
+
+def native_for(group, t):
+    """The native exchange serves this group and CUDA tensor."""
+    if not (t.is_cuda and _NATIVE["group"] is group):
+        return False
+    L = _lib()._lib
+    return hasattr(L, "gsr_dp_world") and L.gsr_dp_world() == dist.get_world_size(group)
+
+
+def finalize_native():
+    C = _lib()
+    if hasattr(C._lib, "gsr_dp_finalize"):
+        C._check(C._lib.gsr_dp_finalize())
+    _NATIVE["group"] = _UNSET
+
+
+class _NativeTicket:
+    """wait() orders the current stream after a native exchange (gsr_dp_wait); keeps the
+    tensors the exchange reads or writes alive until then."""
+
+    def __init__(self, ticket, keep):
+        self.ticket, self.keep = ticket, keep
+
+    def wait(self):
+        if self.ticket is not None:
+            C = _lib()
+            C._check(C._lib.gsr_dp_wait(self.ticket, torch.cuda.current_stream().cuda_stream))
+        self.ticket, self.keep = None, None
+
+    def __del__(self):
+        if getattr(self, "ticket", None) is not None:
+            try:
+                self.wait()
+            except Exception:
+                pass
+
+
+def allreduce_async(t, group=None):
+    """In-place sum of the fp32 tensor t over the group, asynchronous: a handle whose wait()
+    orders the current stream after it (native when init_native set it up, else
+    torch.distributed)."""
+    if native_for(group, t) and t.dtype == torch.float32 and t.is_contiguous():
+        C = _lib()
+        tk = C._lib.gsr_dp_allreduce(t.data_ptr(), t.numel(), torch.cuda.current_stream(t.device).cuda_stream)
+        if tk < 0:
+            raise RuntimeError(C._lib.gsr_last_error().decode())
+        return _NativeTicket(tk, (t,))
+    return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
+
+
 def _all_gather_flat(out, inp, group, async_op):
     """all_gather into one flat buffer (RCCL: all_gather_into_tensor; gloo: list form)."""
     if dist.get_backend(group) == "nccl":
@@ -259,6 +347,18 @@ class ShExchange:
         rest = arena.narrow(0, o_rest, lay["bucket"][1] - o_rest)
         rows_all = torch.empty(world * rows.numel(), dtype=rows.dtype, device=rows.device)
         cuda = rows.is_cuda
+        if self._sh_backward is None and native_for(self.group, rows):
+            # one C call: the collectives as one RCCL group + the dsh rebuild, on the library's stream
+            C = _lib()
+            tk = C._lib.gsr_dp_sh_exchange(P, e["degree"], M, C.NUM_CLASS, e["means3D"].data_ptr(), e["B"],
+                                           arena.data_ptr(), rows.data_ptr(), rows_all.data_ptr(),
+                                           torch.cuda.current_stream(rows.device).cuda_stream)
+            if tk < 0:
+                raise RuntimeError(C._lib.gsr_last_error().decode())
+            if HOST_TIMES is not None:
+                HOST_TIMES["native"] = HOST_TIMES.get("native", 0.0) + time.perf_counter() - t0
+                HOST_TIMES["n"] = HOST_TIMES.get("n", 0) + 1
+            return (_NativeTicket(tk, (arena, rows, rows_all, e["means3D"], e["sh"])), None, e)
         # (torch's _coalescing_manager around these three left rows_all unfilled on RCCL at
         # world size 1 -- tests/test_gpu_dist.py caught it: three calls)
         t1 = time.perf_counter() if HOST_TIMES is not None else 0.0
@@ -321,7 +421,9 @@ class _ShExchangeHandle:
     def wait(self):
         parts, self.parts = self.parts, []
         for ev, _, e in parts:
-            if ev is not None:
+            if isinstance(ev, _NativeTicket):
+                ev.wait()
+            elif ev is not None:
                 torch.cuda.current_stream().wait_event(ev)
             _check_leaf_grads(e)
 
@@ -331,7 +433,10 @@ class _ShExchangeHandle:
         for ev, _, _ in getattr(self, "parts", []):
             if ev is not None:
                 try:
-                    torch.cuda.current_stream().wait_event(ev)
+                    if isinstance(ev, _NativeTicket):
+                        ev.wait()
+                    else:
+                        torch.cuda.current_stream().wait_event(ev)
                 except Exception:
                     pass
         self.parts = []

@@ -279,9 +279,14 @@ def main():
             dist.init_process_group(backend, device_id=device)
         else:
             dist.init_process_group(backend)
+    native_dp = False
 
     from gsr_tools.scene import config_scene_and_camera
     from gsr_tools import dp
+    if dist is not None:
+        # the exchange's collectives from C over the library's own RCCL communicator (csrc/dp.hip;
+        # GSR_NATIVE_DP=0: torch.distributed's calls)
+        native_dp = dp.init_native()
     import diff_gaussian_rasterization as dgr
     from diff_gaussian_rasterization import _C
 
@@ -340,7 +345,7 @@ def main():
         if ex is not None:
             h = ex.start()
         else:
-            h = dist.all_reduce(dp.bucket(dp.arena_of(g[0]), P, shs.shape[1]), op=dist.ReduceOp.SUM, async_op=True)
+            h = dp.allreduce_async(dp.bucket(dp.arena_of(g[0]), P, shs.shape[1]))
         pending.append((h, g))
 
     def drain():
@@ -568,6 +573,8 @@ def main():
         "roofline": roof,
         "stages": stages,
         "exchange": ({"chosen": step.exchange, "mode": args.exchange, "model_us": step.exchange_model,
+                      "issued_by": ("gsr_dp_* over libgsr's own RCCL communicator (csrc/dp.hip)" if native_dp
+                                    else "torch.distributed"),
                       "modelled_choice": getattr(step, "exchange_modelled", None),
                       "trial_ms_per_step": getattr(step, "exchange_trial_ms", None),
                       "model": "gsr_tools/dp.py exchange_cost: ring bytes over world-1 xGMI links at "

@@ -234,6 +234,31 @@ GSR_API int gsr_backward_multiview_deferred_sh(int B, const gsr_view_state* view
 GSR_API int gsr_sh_backward(int V, int P, int D, int M, const float* shs, const float* means3D,
                             const float* sh_rows, float* dsh, float* dmeans3D, void* stream);
 
+/* ---- native data-parallel exchange over RCCL (csrc/dp.hip).  The collectives of the
+ * view-parallel trainer issued from C: one call orders the library's
+ * communication stream after the caller's stream, issues the collectives as one RCCL group (and,
+ * for the SH exchange, the dsh rebuild behind them) and returns a ticket; gsr_dp_wait(ticket,
+ * stream) orders a stream after all of it.  A ticket stays valid for 16 later exchanges.
+ * librccl is loaded at the first gsr_dp_get_unique_id / gsr_dp_init.  The communicator is the
+ * library's own: rank 0 calls gsr_dp_get_unique_id (gsr_dp_unique_id_bytes() bytes), the caller
+ * broadcasts them (e.g. torch.distributed), and every rank calls gsr_dp_init on its device.
+ * gsr_dp_allreduce: in-place float sum of buf [n] over the ranks.
+ * gsr_dp_sh_exchange: the SH exchange of one step (gsr_sh_backward above): sums the arena's
+ * dmeans3D block and its [dopacity .. bucket end) blocks (include/gsr_train.h layout for P, M, C),
+ * all-gathers each rank's views_per_rank views of rows [gsr_sh_rows_floats(P)] into rows_all
+ * [world][views_per_rank][...] and rebuilds the arena's dsh block from them.  The caller keeps
+ * arena, rows, rows_all and means3D alive and unread until it has waited on the ticket.
+ * Both return the ticket (>= 0) or -1 (gsr_last_error()). */
+GSR_API size_t gsr_dp_unique_id_bytes(void);
+GSR_API int gsr_dp_get_unique_id(void* out);
+GSR_API int gsr_dp_init(const void* unique_id, int world, int rank);
+GSR_API int gsr_dp_world(void);  /* 0 before gsr_dp_init / after gsr_dp_finalize */
+GSR_API int gsr_dp_finalize(void);
+GSR_API int gsr_dp_allreduce(float* buf, size_t n, void* stream);
+GSR_API int gsr_dp_sh_exchange(int P, int D, int M, int C, const float* means3D, int views_per_rank, float* arena,
+                               const float* rows, float* rows_all, void* stream);
+GSR_API int gsr_dp_wait(int ticket, void* stream);
+
 /* ---- frustum visibility: present[i] = (view-space z > 0.2).  Replaces
  * markVisible (rasterize_points.cu:223-242, rasterizer_impl.cu:54-66). */
 GSR_API int gsr_mark_visible(int P, const float* means3D, const float* viewmatrix, const float* projmatrix,

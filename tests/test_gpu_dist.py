@@ -65,7 +65,7 @@ def _grad(leaves, view):
     return g
 
 
-def _worker(rank, world, port, backend, out_q):
+def _worker(rank, world, port, backend, out_q, native=False):
     import torch.distributed as dist
     try:
         torch.cuda.set_device(0)
@@ -80,6 +80,9 @@ def _worker(rank, world, port, backend, out_q):
         ref = {k: sum(g[i] for g in gs) for i, k in enumerate(NAMES)}
         ref_m2 = gs[rank][-1]
         res = {"backend": str(dist.get_backend())}
+        # native: the exchanges below go through csrc/dp.hip (gsr_dp_*, libgsr's own RCCL
+        # communicator) instead of torch.distributed's calls
+        res["native"] = dp.init_native() if native else False
 
         # 1. bucket all-reduce over the backward's gradient arena
         g = _grad(leaves, views[rank])
@@ -87,6 +90,12 @@ def _worker(rank, world, port, backend, out_q):
         torch.cuda.synchronize()
         res["allreduce"] = {k: float((a - ref[k]).abs().max()) for k, a in zip(NAMES, g)}
         res["allreduce_m2_equal"] = bool(torch.equal(g[-1], ref_m2))
+        # 1b. the same through dp.allreduce_async (native when set up): bit-exact as well
+        g = _grad(leaves, views[rank])
+        h = dp.allreduce_async(dp.bucket(dp.arena_of(g[0]), P, M))
+        h.wait()
+        torch.cuda.synchronize()
+        res["allreduce_async"] = {k: float((a - ref[k]).abs().max()) for k, a in zip(NAMES, g)}
 
         # 2. ShExchange around torch.autograd.grad
         ex = dp.ShExchange()
@@ -125,6 +134,8 @@ def _worker(rank, world, port, backend, out_q):
         bucket = dp.bucket(dp.arena_of(_grad(leaves, views[rank])[0]), P, M)
         res["bucket_floats"] = int(bucket.numel())
         dist.barrier()
+        if res["native"]:
+            dp.finalize_native()
         dist.destroy_process_group()
         out_q.put((rank, res, None))
     except Exception as e:  # report instead of hanging the parent on the queue
@@ -140,12 +151,14 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("backend,world", [("gloo", 2), ("nccl", 1)])
-def test_ranks_real_backward_exchange(gpu_available, backend, world):
+@pytest.mark.parametrize("backend,world,native", [("gloo", 2, False), ("nccl", 1, False), ("nccl", 1, True)])
+def test_ranks_real_backward_exchange(gpu_available, backend, world, native):
+    """native=True: the exchanges issued by csrc/dp.hip over libgsr's own RCCL communicator
+    (include/gsr.h gsr_dp_*), checked against the same sums."""
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, backend, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, backend, q, native)) for r in range(world)]
     for p in procs:
         p.start()
     try:
@@ -159,8 +172,10 @@ def test_ranks_real_backward_exchange(gpu_available, backend, world):
         assert err is None, f"rank {rank} failed:\n{err}"
     for rank, r, _ in res:
         assert r["backend"] == backend
-        for k, e in r["allreduce"].items():
-            assert e == 0.0, f"rank {rank} allreduce {k}: max |diff| {e:.3e}"
+        assert r["native"] == native, "native exchange not set up"
+        for mode in ("allreduce", "allreduce_async"):
+            for k, e in r[mode].items():
+                assert e == 0.0, f"rank {rank} {mode} {k}: max |diff| {e:.3e}"
         for mode in ("sh_grad", "sh_backward"):
             for k, e in r[mode].items():
                 assert e <= 1e-6, f"rank {rank} {mode} {k}: normwise error {e:.2e}"

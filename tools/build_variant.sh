@@ -16,7 +16,7 @@ for a in "$@"; do
   esac
 done
 srcs=()
-for f in api.hip preprocess.hip binning.hip binning_rows.hip render.hip train.hip knn.hip; do
+for f in api.hip preprocess.hip binning.hip binning_rows.hip render.hip train.hip knn.hip dp.hip; do
   if [ -n "${sub[$f]}" ]; then cp "${sub[$f]}" $C/.variant_$f; srcs+=($C/.variant_$f); else srcs+=($C/$f); fi
 done
 mkdir -p build/variants

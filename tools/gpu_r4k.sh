@@ -1,0 +1,6 @@
+#!/bin/bash
+set -o pipefail
+cd "$(dirname "$0")/.."
+export TMPDIR=/tmp
+PARITY_K="list_segments or c1_config" bash tools/gpu_abv.sh 2 || exit 1
+bash tools/opt_sweep.sh "" "split_fwd_bucket=7" "split_fwd_bucket=9"
