@@ -1109,11 +1109,12 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k
 }
 
 // No split (split_bwd_depth = 0): one wave per block and tile, deepest first.
-// 5 waves per SIMD (96 VGPRs): the compiler spills ~11 values that live across a batch,
-// reloaded once per batch, and the kernel runs 2.8% faster than at 4 waves without spills
-// (rocprofv3 kernel stats, profiles/round4_bwd_waves.txt)
+// Waves per SIMD.  With one wave per tile, 5 (96 VGPRs, ~11 values spilled and reloaded once per
+// batch) ran 2.8% faster than 4 (profiles/round4_bwd_waves.txt); with list segments, whose
+// entries are shorter and twice as many, 4 waves (no spills) run 1.5% faster than 5
+// (k_render_bwd1 350.3 / 349.9 vs 354.7 / 356.8 us, profiles/round4_bwd_segments.txt).
 #ifndef GSR_BWD1_WAVES
-#define GSR_BWD1_WAVES 5
+#define GSR_BWD1_WAVES 4
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD1_WAVES))) k_render_bwd1(
     int W, int H, int gx, int T, uint32_t* __restrict__ sched,
