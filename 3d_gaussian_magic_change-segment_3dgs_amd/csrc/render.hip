@@ -574,8 +574,10 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
 // 0.206 ms without; n >= 2048: 0.222, >= 1024: 0.233, >= 512: 0.246, >= 256: 0.241): each quarter
 // wave repeats the batch loads, the prefilter and the per-instance record reads and ballots for
 // one 8x8 quadrant (profiles/round3_quarter_sweep.txt).
+// Waves per SIMD: 4 measured 1.4% faster than 5 (render_fwd 193.6 / 193.8 vs 195.9 / 197.1 us
+// with list-segment checkpoints, profiles/round4_bwd_segments.txt); 6-8 were slower in round 3.
 #ifndef GSR_FWD_WAVES
-#define GSR_FWD_WAVES 5
+#define GSR_FWD_WAVES 4
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD_WAVES))) k_render_fwd(int W, int H, int gx, int T, const uint32_t* __restrict__ order,
                                                    uint32_t* __restrict__ sched,
@@ -884,25 +886,11 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
             srec[lane][3] = make_float4(rb.z, __uint_as_float(uslot), 0.f, 0.f);  // depth, record slot
             wave_lds_sync();
             uint64_t touched = 0;  // instances with a (partial, SPLIT) record from this wave
-#ifdef GSR_BWD_PREFETCH
-            // the next instance's first two record words are read while this one is replayed
-            float4 nq0 = srec[todo ? (int)__builtin_ctzll(todo) : 0][0];
-            float4 nq1 = srec[todo ? (int)__builtin_ctzll(todo) : 0][1];
-#endif
             while (todo) {
                 const int j = (int)__builtin_ctzll(todo);
                 todo &= todo - 1;
                 const uint32_t p = (uint32_t)(top - 1 - j);
-#ifdef GSR_BWD_PREFETCH
-                const float4 q0 = nq0, q1 = nq1;
-                {
-                    const int jn = todo ? (int)__builtin_ctzll(todo) : 0;
-                    nq0 = srec[jn][0];
-                    nq1 = srec[jn][1];
-                }
-#else
                 const float4 q0 = srec[j][0], q1 = srec[j][1];
-#endif
                 const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
                 float power[NS], dys[NS];
                 uint64_t act[NS];
