@@ -574,8 +574,9 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
 // 0.206 ms without; n >= 2048: 0.222, >= 1024: 0.233, >= 512: 0.246, >= 256: 0.241): each quarter
 // wave repeats the batch loads, the prefilter and the per-instance record reads and ballots for
 // one 8x8 quadrant (profiles/round3_quarter_sweep.txt).
-// Waves per SIMD: 4 measured 1.4% faster than 5 (render_fwd 193.6 / 193.8 vs 195.9 / 197.1 us
-// with list-segment checkpoints, profiles/round4_bwd_segments.txt); 6-8 were slower in round 3.
+// Minimum waves per SIMD for the register allocator: with 4 the kernel still fits 96 VGPRs (5
+// waves/SIMD) but is scheduled differently, and measured 1.4% faster than with 5 (render_fwd
+// 193.6 / 193.8 vs 195.9 / 197.1 us, profiles/round4_bwd_segments.txt); 6-8 were slower in round 3.
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 4
 #endif
