@@ -618,6 +618,9 @@ def main():
         sys.stdout.flush()
         os.write(json_fd, (json.dumps(out) + "\n").encode())
     if dist is not None:
+        if native_dp:
+            torch.cuda.synchronize()
+            dp.finalize_native()  # libgsr's own RCCL communicator (csrc/dp.hip)
         dist.destroy_process_group()
 
 
