@@ -39,7 +39,13 @@ def _worker(rank, world, port, out_q):
     means2D_before = arena.narrow(0, dp.arena_layout(P_TEST, M)["dmeans2D"][0], 3 * P_TEST).clone()
     b = dp.allreduce_bucket(arena, P_TEST, M)
     means2D_after = arena.narrow(0, dp.arena_layout(P_TEST, M)["dmeans2D"][0], 3 * P_TEST)
-    out_q.put((rank, b.numpy().copy(), bool(torch.equal(means2D_before, means2D_after))))
+    # the native exchange stays off on gloo / CPU tensors; dp.allreduce_async then issues
+    # torch.distributed's all-reduce (the same sum, twice: the bucket is already reduced once)
+    native = dp.init_native()
+    b2 = dp.bucket(dp.pack_arena(g, P_TEST, M), P_TEST, M)
+    dp.allreduce_async(b2).wait()
+    out_q.put((rank, b.numpy().copy(), bool(torch.equal(means2D_before, means2D_after)), native,
+               bool(torch.equal(b2, b))))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -70,9 +76,11 @@ def test_view_parallel_allreduce_gloo_ws2():
         g, M = _per_view_grads(view)
         bk = dp.bucket(dp.pack_arena(g, P_TEST, M), P_TEST, M).numpy()
         ref = bk if ref is None else ref + bk
-    for rank, b, m2d_untouched in res:
+    for rank, b, m2d_untouched, native, async_equal in res:
         np.testing.assert_allclose(b, ref, rtol=0, atol=1e-7)
         assert m2d_untouched, "per-view means2D gradients must not be reduced"
+        assert native is False, "the native RCCL exchange must stay off on gloo"
+        assert async_equal, "dp.allreduce_async (torch.distributed fallback) must give the bucket all-reduce"
 
 
 def _stats_worker(rank, world, port, out_q):
