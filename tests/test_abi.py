@@ -149,3 +149,29 @@ def test_binning_capacity_inverts_the_size_query():
         assert L.gsr_binning_capacity(b - 1) < I or I == 0
     t = torch.empty(L.gsr_binning_bytes(5000), dtype=torch.uint8)
     assert _C.binning_capacity(t) >= 5000 and _C.binning_capacity(torch.empty(0, dtype=torch.uint8)) == 0
+
+
+def test_native_exchange_reports_errors_before_init():
+    """The native exchange (csrc/dp.hip, include/gsr.h gsr_dp_*) fails loudly through
+    gsr_last_error when it is used before gsr_dp_init or with bad arguments; none of these
+    paths loads librccl or touches the device."""
+    from diff_gaussian_rasterization import _C
+    L = _C._lib
+    assert L.gsr_dp_world() == 0
+    assert L.gsr_dp_unique_id_bytes() == 128  # sizeof(ncclUniqueId)
+    assert L.gsr_dp_finalize() == 0  # finalize without init is a no-op
+    assert L.gsr_dp_get_unique_id(None) != 0 and b"null unique-id" in L.gsr_last_error()
+    uid = ctypes.create_string_buffer(128)
+    for world, rank in ((0, 0), (1, 1), (2, -1)):
+        assert L.gsr_dp_init(uid, world, rank) != 0 and b"bad unique id" in L.gsr_last_error()
+    assert L.gsr_dp_init(None, 1, 0) != 0
+    assert L.gsr_dp_allreduce(None, 16, None) == -1 and b"null buffer" in L.gsr_last_error()
+    assert L.gsr_dp_allreduce(None, 0, None) == -1 and b"not initialised" in L.gsr_last_error()
+    assert L.gsr_dp_sh_exchange(10, 4, 16, 2, 16, 1, 16, 16, 16, None) == -1
+    assert b"bad P / D / M / C" in L.gsr_last_error()
+    assert L.gsr_dp_sh_exchange(10, 3, 16, 2, None, 1, 16, 16, 16, None) == -1
+    assert b"null argument" in L.gsr_last_error()
+    assert L.gsr_dp_sh_exchange(0, 3, 16, 2, None, 1, None, None, None, None) == -1
+    assert b"not initialised" in L.gsr_last_error()
+    for t in (-1, 0, 16):
+        assert L.gsr_dp_wait(t, None) != 0 and b"bad ticket" in L.gsr_last_error()
