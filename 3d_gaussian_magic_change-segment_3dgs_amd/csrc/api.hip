@@ -851,7 +851,7 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
                          void* geom, void* binning, void* img, void* dst, void* stream) {
     using namespace gsr;
     g_last_error.clear();
-    if (!name || !dst) {
+    if (!name) {
         fail("[gsr] debug_copy: null argument");
         return -1;
     }
@@ -863,9 +863,9 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
     const size_t T = (size_t)IL.gx * IL.gy;
     const char* src = nullptr;
     size_t bytes = 0;
-    auto G = [&](size_t off, size_t b) { if (geom) { src = aligned_base(geom) + off; bytes = b; } };
-    auto B = [&](size_t off, size_t b) { if (binning) { src = aligned_base(binning) + off; bytes = b; } };
-    auto M = [&](size_t off, size_t b) { if (img) { src = aligned_base(img) + off; bytes = b; } };
+    auto G = [&](size_t off, size_t b) { bytes = b; if (geom) src = aligned_base(geom) + off; };
+    auto B = [&](size_t off, size_t b) { bytes = b; if (binning) src = aligned_base(binning) + off; };
+    auto M = [&](size_t off, size_t b) { bytes = b; if (img) src = aligned_base(img) + off; };
     if (n == "tiles_touched") G(GL.tiles_touched, Pz * 4);
     else if (n == "rec") G(GL.rec, Pz * 64);
     else if (n == "clamped") G(GL.clamped, Pz);
@@ -877,9 +877,12 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
     else if (n == "ranges") M(IL.ranges, T * 8);
     else if (n == "n_contrib_tiles") M(IL.n_contrib, T * TILE_PIX * 4);
     else if (n == "tile_order") M(IL.order, tile_sched_words(T) * 4);  // heavy-first order + TileSched
-    else return -1;
-    if (bytes == 0) return 0;
-    if (!src) return -1;
+    else {
+        fail("[gsr] debug_copy: unknown field");
+        return -1;
+    }
+    if (!dst) return (long long)bytes;  // size query: no device access
+    if (bytes == 0 || !src) return 0;   // empty, or the buffer holding it was not passed
     if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess) return -1;
     return (long long)bytes;
 }

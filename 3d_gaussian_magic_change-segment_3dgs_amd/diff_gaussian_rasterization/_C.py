@@ -164,7 +164,13 @@ def debug_state(name, P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffe
     gsr_debug_copy in include/gsr.h).  Unsigned arrays are returned as int32."""
     dtype, per, unit = _DEBUG_FIELDS[name]
     T = ((W + 15) // 16) * ((H + 15) // 16)
-    n = {"P": P, "I": num_rendered, "T": T, "T+": T + 4 + 64 + T + 64 * 2 * T}[unit] * per
+    if unit == "T+":  # the schedule's length is the library's (gsr_internal.h TileSched): ask it
+        nb = int(_lib.gsr_debug_copy(name.encode(), P, W, H, num_rendered, 0, None, None, None, None, None))
+        if nb < 0:
+            raise RuntimeError(f"gsr_debug_copy({name}) size query failed: {_lib.gsr_last_error().decode()}")
+        n = nb // 4
+    else:
+        n = {"P": P, "I": num_rendered, "T": T}[unit] * per
     dev = geomBuffer.device
     out = torch.empty(max(n, 1), dtype=dtype, device=dev)
     ptr = lambda t: t.data_ptr() if t is not None and t.numel() else None

@@ -272,8 +272,10 @@ GSR_API int gsr_mark_visible(int P, const float* means3D, const float* viewmatri
  * "n_contrib_tiles" u32[T,256] (tile-major, in the forward's 8x8-quadrant layout:
  * entry k*64+l of tile (tx, ty) is pixel (16*tx + 8*(k&1) + (l&7), 16*ty + 8*(k>>1) + (l>>3)),
  * k = 0..3 the quadrant, l = 0..63 the lane), "written" u8[I] (after a backward: 1 at
- * every instance slot the render backward stored a gradient record for).  Returns the byte
- * count copied, or -1. */
+ * every instance slot the render backward stored a gradient record for), "tile_order" u32[]
+ * (the heavy-first tile order followed by the render schedule words).  Returns the byte count
+ * copied (0 when the buffer holding the field is NULL), or -1; with dst = NULL, the byte count
+ * a copy would take, without touching the device (callers size dst with it). */
 GSR_API long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered, int binning_capacity,
                                  void* geom, void* binning, void* img, void* dst, void* stream);
 

@@ -101,6 +101,24 @@ def test_errors_reported_without_touching_the_device():
     rc = L.gsr_forward_geometry(ctypes.byref(s), ctypes.byref(inp), None, None, None, ctypes.byref(nr))
     assert rc != 0 and b"SH degree" in L.gsr_last_error()
     assert L.gsr_debug_copy(b"no_such_field", 1, 16, 16, 0, 0, None, None, None, 16, None) == -1
+    assert b"unknown field" in L.gsr_last_error()
+
+
+def test_debug_copy_size_query():
+    """gsr_debug_copy with dst = NULL returns the bytes a copy would take (no device access):
+    the parity tests size their copies with it, so the host never assumes the library's layout."""
+    from diff_gaussian_rasterization import _C
+    L = _C._lib
+    q = lambda name, P=7, W=100, H=40, I=33: L.gsr_debug_copy(name.encode(), P, W, H, I, 0,  # noqa: E731
+                                                              None, None, None, None, None)
+    T = 7 * 3
+    assert q("rec") == 7 * 64 and q("point_list") == 33 * 4 and q("ranges") == T * 8
+    assert q("n_contrib_tiles") == T * 256 * 4 and q("written") == 33
+    sched = q("tile_order")
+    assert sched % 4 == 0 and sched // 4 >= 2 * T + 4 + 64 + 64 * T  # order, sched words, counts, lists
+    assert q("no_such_field") == -1
+    # a field whose buffer is not passed copies nothing
+    assert L.gsr_debug_copy(b"rec", 7, 100, 40, 33, 0, None, None, None, 16, None) == 0
 
 
 def test_python_api_rejects_cpu_tensors():
