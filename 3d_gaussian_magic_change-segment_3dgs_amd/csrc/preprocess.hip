@@ -16,6 +16,12 @@
 
 #include "gsr_internal.h"
 
+// Two translation units: this file (GSR_PRE_PART 1) and gaussian_bwd.hip, which includes it
+// for k_gaussian_backward alone (2), built with its own machine-scheduler strategy (Makefile).
+#ifndef GSR_PRE_PART
+#define GSR_PRE_PART 1
+#endif
+
 namespace gsr {
 namespace {
 
@@ -573,6 +579,7 @@ __device__ __forceinline__ void sum_records(const float* __restrict__ contrib, c
     for (int j = 0; j < 12; ++j) q[j] = (float)d[j];
 }
 
+#if GSR_PRE_PART == 2
 // ----------------------------------------------------------------- backward --
 // One thread per Gaussian.  Sums the per-(tile, Gaussian) gradient records that
 // the render backward wrote at the Gaussian's instance slots (replacing the
@@ -887,6 +894,8 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
 }
 
 
+#endif  // GSR_PRE_PART == 2
+#if GSR_PRE_PART == 1
 // ------------------------------------------------------- multi-view backward --
 // Parameter gradients of B views summed (gsr_backward_multiview).  Two kernels:
 //  k_gaussian_backward_mv: per Gaussian, loops over the views: record gather,
@@ -1176,8 +1185,10 @@ __global__ void __launch_bounds__(256) k_sh_dsh(int P, int D, int M, const float
         for (int f = 0; f < 3 * M; ++f) o[f] = f < 48 ? acc[f] : 0.f;
     }
 }
+#endif  // GSR_PRE_PART == 1
 }  // namespace
 
+#if GSR_PRE_PART == 1
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec, int* radii,
                        uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped, ushort4* rect,
                        uint32_t* rect32, float* shjac, void* zero_a, size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes,
@@ -1213,7 +1224,9 @@ void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const 
     else
         hipLaunchKernelGGL(k_sh_dsh<false>, dim3(cdiv(P, 256)), dim3(256), 0, st, P, D, M, means3D, V, shx, dsh);
 }
+#endif  // GSR_PRE_PART == 1
 
+#if GSR_PRE_PART == 2
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
                               const float* contrib, const uint8_t* written, const float4* rec,
@@ -1222,5 +1235,7 @@ void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const
     hipLaunchKernelGGL(k_gaussian_backward, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, radii, tiles_touched,
                        goff, clamped, contrib, written, rec, shjac, g, in.shs ? shx : nullptr);
 }
+
+#endif  // GSR_PRE_PART == 2
 
 }  // namespace gsr

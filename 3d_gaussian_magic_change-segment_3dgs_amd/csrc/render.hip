@@ -38,6 +38,18 @@
 // mean2D / conic gradients with the Gaussian's own conic and opacity.
 #include "gsr_internal.h"
 
+// Two translation units: this file's forward part (GSR_RENDER_PART 1) and render_bwd.hip,
+// which includes it for the backward part (2), each built with its own machine-scheduler
+// strategy (Makefile).  Diagnostic builds (GSR_WAVE_TRACE / GSR_STATS, whose trace buffers
+// are per translation unit) compile both parts here (0).
+#ifndef GSR_RENDER_PART
+#if defined(GSR_WAVE_TRACE) || defined(GSR_STATS)
+#define GSR_RENDER_PART 0
+#else
+#define GSR_RENDER_PART 1
+#endif
+#endif
+
 #include <type_traits>
 
 // Numerics.  The blend thresholds alpha >= 1/255 and T*(1-alpha) >= 1e-4
@@ -577,6 +589,7 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
 // Minimum waves per SIMD for the register allocator: with 4 the kernel still fits 96 VGPRs (5
 // waves/SIMD) but is scheduled differently, and measured 1.4% faster than with 5 (render_fwd
 // 193.6 / 193.8 vs 195.9 / 197.1 us, profiles/round4_bwd_segments.txt); 6-8 were slower in round 3.
+#if GSR_RENDER_PART != 2
 #ifndef GSR_FWD_WAVES
 #define GSR_FWD_WAVES 4
 #endif
@@ -608,6 +621,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD
                     out_alpha, out_segment, n_contrib, ckpt, ck, srec);
     }
 }
+#endif  // GSR_RENDER_PART != 2
 
 template <int CTRL>
 __device__ __forceinline__ float dpp(float v) {
@@ -1056,6 +1070,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
     WT_END(1, wslot, tile, n, top0, NS)
 }
 
+#if GSR_RENDER_PART != 1
 // The backward walks the forward's depth queue deepest first (TileSched): global work
 // index i -> bucket (a wave prefix over the 63 bucket counts, descending) -> tile.  Tiles
 // at least split_depth deep come first, one per block (top / bottom half on wave 0 / 1);
@@ -1152,8 +1167,10 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD
                        kind == BQ_FRONT ? ckpt : nullptr);
 }
 
+#endif  // GSR_RENDER_PART != 1
 }  // namespace
 
+#if GSR_RENDER_PART != 2
 void set_bwd_ckpt(int pos) { g_bwd_ckpt = pos > 0 ? (pos + 63) / 64 * 64 : 0; }
 int bwd_ckpt() { return g_bwd_ckpt; }
 
@@ -1170,7 +1187,9 @@ void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, 
                        sched, ranges, point_list,
                        rec, bg, out_color, out_depth, out_alpha, out_segment, n_contrib, ckpt, ck);
 }
+#endif  // GSR_RENDER_PART != 2
 
+#if GSR_RENDER_PART != 1
 void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
                             const uint2* ranges, const uint32_t* point_list, const uint32_t* slot_vals,
                             const float4* rec, const float* bg, const float* alpha, const uint32_t* n_contrib,
@@ -1192,5 +1211,7 @@ void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order,
                        slot_vals, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib,
                        written);
 }
+
+#endif  // GSR_RENDER_PART != 1
 
 }  // namespace gsr
