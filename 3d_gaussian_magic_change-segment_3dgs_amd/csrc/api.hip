@@ -705,6 +705,19 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
     const int P = s0->P;
     if (P == 0) return 0;
     if (in->shs && !mv_scratch && !defer) return fail("[gsr] multiview: scratch is NULL");
+    // Every view is validated before any work is queued: once odd views run on the auxiliary
+    // stream, an early return would leave the caller's stream unordered after work that still
+    // reads and writes the caller's buffers.
+    for (int v = 0; v < B; ++v) {
+        const gsr_view_state& V = views[v];
+        if (!V.geom || !V.img || !V.radii || !V.alpha || !V.dL_dcolor || !V.dL_dsegment || !V.dL_ddepth ||
+            !V.dL_dalpha)
+            return fail("[gsr] multiview: null buffer");
+        // each view's SH direction Jacobian comes from its forward (as in gsr_backward)
+        if (int rc = check_source(V.geom, P, in->shs != nullptr)) return rc;
+        if (V.num_rendered > 0 && (!V.binning || !V.scratch))
+            return fail("[gsr] multiview: binning/scratch buffer is NULL");
+    }
     hipStream_t st = (hipStream_t)stream;
     const bool dbg = s0->debug != 0;
     hipStream_t aux = (B > 1 && g_mv_streams && !dbg) ? aux_stream() : nullptr;
@@ -713,16 +726,16 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
                 hipStreamWaitEvent(aux, fj->fork, 0) != hipSuccess))
         aux = nullptr;
     bool aux_used = false;
+    // a failure after the fork still joins: the caller's stream waits for the auxiliary work
+    auto join = [&]() -> bool {
+        return !aux || !aux_used ||
+               (hipEventRecord(fj->join, aux) == hipSuccess && hipStreamWaitEvent(st, fj->join, 0) == hipSuccess);
+    };
     MvArgs a{};
     a.B = B;
     for (int v = 0; v < B; ++v) {
         const gsr_view_state& V = views[v];
         const gsr_settings* s = V.s;
-        if (!V.geom || !V.img || !V.radii || !V.alpha || !V.dL_dcolor || !V.dL_dsegment || !V.dL_ddepth ||
-            !V.dL_dalpha)
-            return fail("[gsr] multiview: null buffer");
-        // each view's SH direction Jacobian comes from its forward (as in gsr_backward)
-        if (int rc = check_source(V.geom, P, in->shs != nullptr)) return rc;
         const size_t I = V.num_rendered > 0 ? (size_t)V.num_rendered : 0;
         const ImgLayout IL = img_layout(s->W, s->H);
         char* im = aligned_base(V.img);
@@ -731,7 +744,6 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
         float* contrib = nullptr;
         uint8_t* written = nullptr;
         if (I > 0) {
-            if (!V.binning || !V.scratch) return fail("[gsr] multiview: binning/scratch buffer is NULL");
             const BinLayout BL = bin_layout(bin_cap(V.s, I));
             char* b = aligned_base(V.binning);
             contrib = reinterpret_cast<float*>(aligned_base(V.scratch));
@@ -747,7 +759,10 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
                                        at<uint32_t>(im, IL.n_contrib), V.dL_dcolor, V.dL_dsegment, V.dL_ddepth,
                                        V.dL_dalpha, contrib, written, at<float>(im, IL.ckpt), sv);
             }
-            if (int rc = check("render backward", sv, dbg)) return rc;
+            if (int rc = check("render backward", sv, dbg)) {
+                (void)join();
+                return rc;
+            }
         } else {
             // nothing rendered: every radius is 0 and the records are never read
             written = nullptr;
@@ -770,13 +785,9 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
         w.tanfovx = s->tanfovx;
         w.tanfovy = s->tanfovy;
     }
-    if (aux) {  // join: the per-Gaussian pass (and the caller) after every view's render backward
-        if (!aux_used) {
-            // nothing went to the auxiliary stream (e.g. the odd views rendered nothing)
-        } else if (hipEventRecord(fj->join, aux) != hipSuccess || hipStreamWaitEvent(st, fj->join, 0) != hipSuccess) {
-            return fail("[gsr] multiview: stream join failed");
-        }
-    }
+    // join: the per-Gaussian pass (and the caller) after every view's render backward (nothing to
+    // join when no view went to the auxiliary stream, e.g. the odd views rendered nothing)
+    if (!join()) return fail("[gsr] multiview: stream join failed");
     {
         StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);
         float* shx = defer ? sh_rows : reinterpret_cast<float*>(in->shs ? aligned_base(mv_scratch) : nullptr);

@@ -85,6 +85,20 @@ int nccl_check(const Rccl& r, ncclResult_t e, const char* what) {
     return dp_fail(std::string(what) + ": " + (r.ErrorString ? r.ErrorString(e) : "error"));
 }
 
+// Destroy the communicator, the stream and the events (whichever exist); the state is then
+// uninitialised.  Caller holds s.mu.
+ncclResult_t release(DpState& s) {
+    ncclResult_t e = ncclSuccess;
+    if (s.comm) e = s.r.CommDestroy(s.comm);
+    s.comm = nullptr;
+    for (int i = 0; i < DP_TICKETS; ++i)
+        if (s.done[i]) (void)hipEventDestroy(s.done[i]), s.done[i] = nullptr;
+    if (s.ready) (void)hipEventDestroy(s.ready), s.ready = nullptr;
+    if (s.cs) (void)hipStreamDestroy(s.cs), s.cs = nullptr;
+    s.world = 0;
+    return e;
+}
+
 // Order the communication stream after `stream`'s work so far.
 int dp_begin(DpState& s, hipStream_t stream) {
     if (!s.comm) return dp_fail("not initialised (gsr_dp_init)");
@@ -144,14 +158,22 @@ int gsr_dp_init(const void* unique_id, int world, int rank) {
     bool ok = hipStreamCreateWithFlags(&s.cs, hipStreamNonBlocking) == hipSuccess &&
               hipEventCreateWithFlags(&s.ready, hipEventDisableTiming) == hipSuccess;
     for (int i = 0; ok && i < DP_TICKETS; ++i) ok = hipEventCreateWithFlags(&s.done[i], hipEventDisableTiming) == hipSuccess;
-    if (!ok) return dp_fail("stream / event creation failed");
+    if (!ok) {
+        // leave nothing half-initialised: a retry starts from scratch
+        release(s);
+        return dp_fail("stream / event creation failed");
+    }
     s.world = world;
     s.rank = rank;
     s.next = 0;
     return 0;
 }
 
-int gsr_dp_world(void) { return gsr::dp().comm ? gsr::dp().world : 0; }
+int gsr_dp_world(void) {
+    gsr::DpState& s = gsr::dp();
+    std::lock_guard<std::mutex> lk(s.mu);
+    return s.comm ? s.world : 0;
+}
 
 int gsr_dp_finalize(void) {
     using namespace gsr;
@@ -160,14 +182,7 @@ int gsr_dp_finalize(void) {
     std::lock_guard<std::mutex> lk(s.mu);
     if (!s.comm) return 0;
     if (s.cs) (void)hipStreamSynchronize(s.cs);
-    const ncclResult_t e = s.r.CommDestroy(s.comm);
-    s.comm = nullptr;
-    for (int i = 0; i < DP_TICKETS; ++i)
-        if (s.done[i]) (void)hipEventDestroy(s.done[i]), s.done[i] = nullptr;
-    if (s.ready) (void)hipEventDestroy(s.ready), s.ready = nullptr;
-    if (s.cs) (void)hipStreamDestroy(s.cs), s.cs = nullptr;
-    s.world = 0;
-    return nccl_check(s.r, e, "ncclCommDestroy");
+    return nccl_check(s.r, release(s), "ncclCommDestroy");
 }
 
 int gsr_dp_allreduce(float* buf, size_t n, void* stream) {
@@ -228,6 +243,8 @@ int gsr_dp_wait(int ticket, void* stream) {
     using namespace gsr;
     (void)set_error("");
     DpState& s = dp();
+    std::lock_guard<std::mutex> lk(s.mu);
+    if (!s.comm) return dp_fail("not initialised (gsr_dp_init)");
     if (ticket < 0 || ticket >= DP_TICKETS || !s.done[ticket]) return dp_fail("bad ticket");
     if (hipStreamWaitEvent((hipStream_t)stream, s.done[ticket], 0) != hipSuccess) return dp_fail("stream wait failed");
     return 0;

@@ -48,6 +48,7 @@ def bucket(arena, P, M):
 def allreduce_bucket(arena, P, M, group=None):
     """Sum the parameter-gradient bucket over all ranks, in place; returns the bucket view."""
     b = bucket(arena, P, M)
+    native_fence()
     dist.all_reduce(b, op=dist.ReduceOp.SUM, group=group)
     return b
 
@@ -68,6 +69,7 @@ def allreduce_model_grad(model, group=None):
     arena gradient has the bucket layout, so this is the same single collective."""
     g = model._arena.grad
     if g is not None:
+        native_fence()
         dist.all_reduce(g, op=dist.ReduceOp.SUM, group=group)
     return g
 
@@ -78,6 +80,7 @@ def reduce_densification_stats(xyz_gradient_accum, denom, max_radii2D, group=Non
     summed, max_radii2D is max-reduced.  Each rank accumulated its own views'
     |dmeans2D| before any reduction, as the reference does per view."""
     both = torch.cat([xyz_gradient_accum.reshape(-1), denom.reshape(-1)])
+    native_fence()
     dist.all_reduce(both, op=dist.ReduceOp.SUM, group=group)
     n = xyz_gradient_accum.numel()
     xyz_gradient_accum.copy_(both[:n].view_as(xyz_gradient_accum))
@@ -177,7 +180,22 @@ def measure_rebuild_us(P, M, views, device, degree=3, reps=5):
 # time per collective; at one view per rank the SH exchange's start then took 130-170 us of a
 # 0.9-ms step and the host bounded the step (profiles/round4_c_rccl_world1_sh.json).
 _UNSET = object()
-_NATIVE = {"group": _UNSET}  # the group init_native set the native path up for
+_NATIVE = {"group": _UNSET, "last": None}  # the group init_native set up; the last ticket issued
+
+
+def native_fence():
+    """Order the current stream after the last native exchange before a torch.distributed
+    collective is issued.  torch's collectives run on the process group's stream, which waits
+    for the current stream, so with this fence no collective of torch's communicator can run
+    beside one of libgsr's: the two communicators' collectives execute in one order on every
+    rank (the native call itself orders its stream after the current stream, csrc/dp.hip
+    dp_begin).  No-op when the native path is off."""
+    t = _NATIVE["last"]
+    if t is None or _NATIVE["group"] is _UNSET:
+        return
+    L = _lib()._lib
+    if torch.cuda.is_initialized() and L.gsr_dp_world() > 0:
+        _lib()._check(L.gsr_dp_wait(t, torch.cuda.current_stream().cuda_stream))
 
 
 def _lib():
@@ -198,6 +216,10 @@ def init_native(group=None):
         return False
     if L.gsr_dp_world() > 0:
         return _NATIVE["group"] is group
+    if dist.get_world_size(group) > 1 and os.environ.get("GSR_NATIVE_DP") is None:
+        # world > 1: the native path is opt-in (GSR_NATIVE_DP=1) until a multi-GPU run has
+        # exercised it; bench.py and the trainer use torch.distributed's collectives otherwise
+        return False
     n = int(L.gsr_dp_unique_id_bytes())
     uid = ctypes.create_string_buffer(n)
     if dist.get_rank(group) == 0:
@@ -223,6 +245,7 @@ def finalize_native():
     if hasattr(C._lib, "gsr_dp_finalize"):
         C._check(C._lib.gsr_dp_finalize())
     _NATIVE["group"] = _UNSET
+    _NATIVE["last"] = None
 
 
 class _NativeTicket:
@@ -255,7 +278,9 @@ def allreduce_async(t, group=None):
         tk = C._lib.gsr_dp_allreduce(t.data_ptr(), t.numel(), torch.cuda.current_stream(t.device).cuda_stream)
         if tk < 0:
             raise RuntimeError(C._lib.gsr_last_error().decode())
+        _NATIVE["last"] = tk
         return _NativeTicket(tk, (t,))
+    native_fence()
     return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group, async_op=True)
 
 
@@ -355,12 +380,14 @@ class ShExchange:
                                            torch.cuda.current_stream(rows.device).cuda_stream)
             if tk < 0:
                 raise RuntimeError(C._lib.gsr_last_error().decode())
+            _NATIVE["last"] = tk
             if HOST_TIMES is not None:
                 HOST_TIMES["native"] = HOST_TIMES.get("native", 0.0) + time.perf_counter() - t0
                 HOST_TIMES["n"] = HOST_TIMES.get("n", 0) + 1
             return (_NativeTicket(tk, (arena, rows, rows_all, e["means3D"], e["sh"])), None, e)
         # (torch's _coalescing_manager around these three left rows_all unfilled on RCCL at
         # world size 1 -- tests/test_gpu_dist.py caught it: three calls)
+        native_fence()
         t1 = time.perf_counter() if HOST_TIMES is not None else 0.0
         works = [dist.all_reduce(xyz, op=dist.ReduceOp.SUM, group=self.group, async_op=True),
                  dist.all_reduce(rest, op=dist.ReduceOp.SUM, group=self.group, async_op=True),

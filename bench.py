@@ -251,6 +251,12 @@ def main():
                          "(all-gather of 3-float dRGB rows + all-reduce of 13 floats, gsr_tools.dp.ShExchange); "
                          "auto = the one with fewer bytes per link for the step's views per rank")
     args = ap.parse_args()
+    from gsr_tools import launch
+    if launch.needs_launch(args.gpus):
+        # `python3 bench.py --gpus N` without torch.distributed.run: start the N ranks here
+        # (children of this process, which never touches the GPU) and relay rank 0's line
+        sys.exit(launch.spawn_ranks(args.gpus, [sys.executable, os.path.abspath(__file__)] + sys.argv[1:],
+                                    env=dict(os.environ, GSR_LAUNCHER="bench.py")))
     # The bench line is the only thing on stdout: native libraries (RCCL prints its version
     # banner at communicator set-up) write to file descriptor 1 directly, so fd 1 is pointed
     # at stderr for the run and the JSON line goes to the saved descriptor.
@@ -262,8 +268,8 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world:
-        if world == 1 and args.gpus > 1:
-            sys.exit("bench.py --gpus N>1 must be launched with torch.distributed.run (one process per GPU)")
+        print(f"[bench] --gpus {args.gpus} under a launcher with WORLD_SIZE={world}: running {world} rank(s)",
+              file=sys.stderr)
     # one process per GPU; on a box with fewer GPUs than ranks (rehearsal runs with
     # GSR_DIST_BACKEND=gloo) ranks share devices round-robin
     dev_index = local_rank % max(1, torch.cuda.device_count())
@@ -569,6 +575,9 @@ def main():
                                                    " per step, overlapped with the next step's render)")
                                                   if dist is not None else ""),
                    "dist_backend": dinfo["backend"], "world_size": dinfo["world_size"],
+                   "launcher": (os.environ.get("GSR_LAUNCHER") or
+                                ("torch.distributed.run" if "TORCHELASTIC_RUN_ID" in os.environ else
+                                 ("env" if "WORLD_SIZE" in os.environ else None))),
                    "rccl_version": dinfo["rccl_version"]},
         "roofline": roof,
         "stages": stages,

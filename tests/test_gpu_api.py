@@ -256,3 +256,40 @@ def test_backward_rejects_sh_after_colors_precomp_forward(gpu_available):
     g = backward(cols, E)
     torch.cuda.synchronize()
     assert torch.isfinite(g[3]).all() and float(g[1].abs().sum()) > 0
+
+
+def test_multiview_backward_rejects_bad_view_before_any_launch(gpu_available):
+    """the multi-view backward puts odd views' render backward on libgsr's auxiliary
+    stream.  A view that fails its checks (here view 2 of 3: a geom buffer from a colors_precomp
+    forward, backward given shs) must fail the call before anything is queued, so no auxiliary
+    work can outlive the call unjoined.  The same three views with a consistent colour source
+    then succeed."""
+    from diff_gaussian_rasterization import _C
+    scene = synthetic_scene(3000, sh_degree=3, seed=73)
+    dev = "cuda"
+    means3D, opac, segs = scene.means3D.to(dev), scene.opacities.to(dev), scene.segments.to(dev)
+    scales, rots, shs = scene.scales.to(dev), scene.rotations.to(dev), scene.shs.to(dev)
+    cols = torch.rand(scene.P, 3, device=dev)
+    E = torch.Tensor([])
+    views = []
+    for v in range(3):
+        cam = orbit_camera(v, 96, 64, 80.0)
+        st = Hn.settings_for(cam, 3, dev)
+        use_cols = v == 2
+        R, color, depth, segment, alpha, radii, geom, binning, img = _C.rasterize_gaussians(
+            st.bg, means3D, cols if use_cols else E, segs, opac, scales, rots, st.scale_modifier, E,
+            st.viewmatrix, st.projmatrix, st.tanfovx, st.tanfovy, st.image_height, st.image_width,
+            E if use_cols else shs, st.sh_degree, st.campos, st.prefiltered, st.debug)
+        assert R > 0
+        views.append(dict(bg=st.bg, viewmatrix=st.viewmatrix, projmatrix=st.projmatrix, tanfovx=st.tanfovx,
+                          tanfovy=st.tanfovy, image_height=st.image_height, image_width=st.image_width,
+                          campos=st.campos, radii=radii, geom=geom, binning=binning, img=img, num_rendered=R,
+                          alpha=alpha, dL_dcolor=torch.randn_like(color), dL_dsegment=torch.randn_like(segment),
+                          dL_ddepth=torch.randn_like(depth), dL_dalpha=torch.randn_like(alpha)))
+    with pytest.raises(RuntimeError, match="colors_precomp"):
+        _C.rasterize_gaussians_backward_multiview(views, means3D, E, segs, scales, rots, 1.0, E, shs, 3, False)
+    torch.cuda.synchronize()
+    out, d2 = _C.rasterize_gaussians_backward_multiview(views[:2], means3D, E, segs, scales, rots, 1.0, E, shs, 3,
+                                                        False)
+    torch.cuda.synchronize()
+    assert torch.isfinite(out[3]).all() and float(out[5].abs().sum()) > 0
