@@ -365,6 +365,10 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
     }
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
+#ifdef GSR_FWD_CK_BY_N
+    // a tile shorter than ck + CK_MIN_BACK is never split (publish_depth): no checkpoint
+    if (n < ck + (int)CK_MIN_BACK) ck = 0;
+#endif
     STAT_DECL
     STAT(7, n);
     // prefilter rectangle: the pixels this wave owns
@@ -906,6 +910,9 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                 todo &= todo - 1;
                 const uint32_t p = (uint32_t)(top - 1 - j);
                 const float4 q0 = srec[j][0], q1 = srec[j][1];
+#ifdef GSR_BWD_EARLY_REC
+                const float4 q2 = srec[j][2], q3 = srec[j][3];  // one LDS wait per instance
+#endif
                 const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
                 float power[NS], dys[NS];
                 uint64_t act[NS];
@@ -944,7 +951,9 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                     continue;
                 }
                 STAT(3, 1);
+#ifndef GSR_BWD_EARLY_REC
                 const float4 q2 = srec[j][2], q3 = srec[j][3];
+#endif
                 const float op = q1.z, dep = q3.x, s0v = q1.w;
 #ifdef GSR_STATS
                 unsigned long long okst_ = st_[12];

@@ -504,7 +504,18 @@ def main():
     stride = 4 if args.steps >= 8 else 1
     elapsed = timed(step, args.steps, step_ms, stride=stride, dom_mask=1 << dom_i)
     _C._lib.gsr_timing_enable(0)
-    ms, cnt = collect()  # the dominant stage's launches inside the timed region
+    ms, cnt = collect()  # the dominant stage's launches inside the timed region (every 4th step)
+    # The dominant kernel's launch time for `roofline`: right after the timed region, the same
+    # steps again with libgsr's event bracket around EVERY launch of that stage (and no other
+    # stage bracketed), so the mean is over every launch of the pass, not a sample.
+    n_kpass = max(1, min(args.steps, 20))
+    _C._lib.gsr_timing_enable(1 << dom_i)
+    for _ in range(n_kpass):
+        step()
+    drain()
+    torch.cuda.synchronize()
+    _C._lib.gsr_timing_enable(0)
+    kms, kcnt = collect()
     I, HW = int(state["I"]), W * H
     Wrec = written_records()  # gradient records the render backward stores (gaussian_bwd's bytes)
     stages = {}
@@ -520,8 +531,9 @@ def main():
     dinfo = dist_info(dist)
     value = world * B * args.steps / elapsed
     roof = None
-    if dom and cnt[dom_i]:
-        avg_live = ms[dom_i] / cnt[dom_i]  # measured inside the timed region
+    if dom and kcnt[dom_i]:
+        avg_live = kms[dom_i] / kcnt[dom_i]  # every launch of the dedicated pass
+        avg_window = ms[dom_i] / cnt[dom_i] if cnt[dom_i] else None  # sampled inside the timed region
         achieved = round(algorithmic_bytes(dom, P, I, HW, deg, B, written=Wrec) / (avg_live * 1e-3) / 1e9, 1)
         traffic = cyc_per_valu = None
         pmc, pmc_note = pmc_for_this_build()
@@ -543,7 +555,15 @@ def main():
                 "measured_copy_peak": measured_peak,
                 "frac_of_measured_peak": round(achieved / measured_peak, 4) if measured_peak else None,
                 "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg, B, written=Wrec),
-                "avg_launch_ms": round(avg_live, 4), "launches_timed": int(cnt[dom_i]),
+                "avg_launch_ms": round(avg_live, 4), "launches_timed": int(kcnt[dom_i]),
+                "timing": (f"mean of hipEvent brackets that libgsr records on its launch stream around every "
+                           f"{dom} launch of {n_kpass} steps run right after the timed region (only that stage "
+                           f"bracketed); the same bracket sampled every 4th step inside the timed region: "
+                           f"avg_launch_ms_timed_region; every stage bracketed (untimed stage pass): "
+                           f"avg_launch_ms_stage_pass; rocprofv3 --kernel-trace --stats of this command: "
+                           f"profiles/round5_*_kernel_stats.csv"),
+                "avg_launch_ms_timed_region": round(avg_window, 4) if avg_window else None,
+                "avg_launch_ms_stage_pass": round(sms[dom_i] / scnt[dom_i], 4) if scnt[dom_i] else None,
                 "valu_instr_per_launch": (pmc.get("kernels", {}).get(dom, {}).get("SQ_INSTS_VALU")
                                           if pmc is not None else None),
                 "pmc_source": pmc_note,
@@ -602,15 +622,40 @@ def main():
         # one multi-view backward and one exchange per step (bigger, fewer collectives
         # for point-to-point xGMI; SURVEY.md s8e / DESIGN.md s7).
         bstep = make_step(BB)
-        for _ in range(max(1, args.warmup // 4)):
+        # its own warm-up: the first batched steps grow the caching allocator's pools on both
+        # streams (BENCH_r04 timed 8 steps after 1 warm-up step: 1.014x; 25 after 2: 1.055x)
+        for _ in range(max(3, args.warmup // 4)):
             bstep()
         drain()
-        k = max(8, args.steps // BB)
+        torch.cuda.synchronize()
+        k = max(16, args.steps // BB)
         el_b = timed(bstep, k)
+        # overlap of the two streams: every stage bracketed (untimed, 3 steps) -> the stage busy
+        # time summed over both streams per step, against the wall time of the same steps
+        collect()
+        _C._lib.gsr_timing_enable(-1)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(3):
+            bstep()
+        drain()
+        torch.cuda.synchronize()
+        wall_b = (time.perf_counter() - t0) / 3
+        _C._lib.gsr_timing_enable(0)
+        bms, _ = collect()
+        busy_b = sum(bms[i] for i in range(nst)) * 1e-3 / 3
         out["batched"] = {"views_per_step_per_gpu": BB, "global_batch": world * BB, "steps": k,
                           "value": round(world * BB * k / el_b, 2), "unit": "views/s",
                           "ms_per_step": round(1e3 * el_b / k, 4),
                           "exchange": bstep.exchange, "exchange_model_us": bstep.exchange_model,
+                          "ratio_to_value": round(world * BB * k / el_b / value, 4),
+                          "overlap": {"stage_busy_us_per_step": round(1e6 * busy_b, 1),
+                                      "wall_us_per_step": round(1e6 * wall_b, 1),
+                                      "busy_over_wall": round(busy_b / wall_b, 3) if wall_b > 0 else None,
+                                      "note": "3 untimed steps with every stage bracketed by libgsr's events on "
+                                              "the stream it launches on (the caller's and the side / auxiliary "
+                                              "stream): busy time summed over both streams; > 1 = the streams "
+                                              "overlapped"},
                           "note": "per-view forward + one gsr_backward_multiview over the batch + one exchange"}
     out["train_step"] = None
     if rank == 0 and world == 1 and not args.no_train:

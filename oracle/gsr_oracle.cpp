@@ -176,6 +176,9 @@ struct State {
     std::vector<uint32_t> point_list; // sorted gaussian ids [I]
     std::vector<uint32_t> ranges;     // [T,2]
     std::vector<uint32_t> n_contrib;  // [H*W]
+    // per pixel: FNV-1a hash of the blend's decision sequence (forward.cu:343-361) -- the list
+    // positions that blend and the one that terminates; equal hashes = identical decisions
+    std::vector<uint64_t> dhash;      // [H*W]
     std::vector<float> alpha;         // out_alpha copy [H*W]
     std::vector<float> segments;      // [P,2] (zeros if absent)
     std::vector<float> gabs;          // [P,12] sum of |per-pixel gradient terms| (after backward)
@@ -291,6 +294,25 @@ static inline float gsr_expf(float x) {
     return p * scale;
 }
 static inline float oracle_exp(float x) { return g_exp_libm ? std::exp(x) : gsr_expf(x); }
+// g_exp_jitter != 0: every blend exp (forward and backward alike) moves by -1 .. +1 ulp, chosen
+// by a hash of (seed, Gaussian, pixel) -- the reference algorithm run with a different faithful
+// exp, to measure each output element's own sensitivity to last-bit alpha differences
+// (tests/test_gpu_exp_budget.py).
+static uint32_t g_exp_jitter = 0;
+static inline float jitter_exp(float G, uint32_t g, uint32_t pix) {
+    if (!g_exp_jitter || !(G > 0.f)) return G;
+    uint64_t h = ((uint64_t)g_exp_jitter << 40) ^ ((uint64_t)g << 20) ^ (uint64_t)pix;
+    h ^= h >> 33;
+    h *= 0xff51afd7ed558ccdull;
+    h ^= h >> 33;
+    h *= 0xc4ceb9fe1a85ec53ull;
+    h ^= h >> 33;
+    // -1 .. +1 ulp
+    int r = (int)(h % 3u) - 1;
+    for (; r < 0; ++r) G = std::nextafter(G, 0.0f);
+    for (; r > 0; --r) G = std::nextafter(G, 2.0f * G);
+    return G;
+}
 // 1: emulate the reference's fp32 accumulation (one fixed order of its atomics)
 static int g_acc32 = 0;
 
@@ -302,6 +324,7 @@ const char* oracle_last_error(void) { return g_err.c_str(); }
 
 void oracle_set_acc32(int on) { g_acc32 = on; }
 void oracle_set_exp_libm(int on) { g_exp_libm = on; }
+void oracle_set_exp_jitter(unsigned seed) { g_exp_jitter = seed; }
 float oracle_expf(float x) { return gsr_expf(x); }
 
 int oracle_num_threads(void) {
@@ -452,6 +475,7 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
 
     // renderCUDA forward (forward.cu:258-392)
     st->n_contrib.assign((size_t)W * H, 0);
+    st->dhash.assign((size_t)W * H, 0);
     st->alpha.assign((size_t)W * H, 0.f);
     const float* feat = in->colors_precomp ? in->colors_precomp : st->rgb.data();
     const float* segs = st->segments.data();
@@ -467,6 +491,10 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
                 const float pfx = (float)px, pfy = (float)py;
                 float Tr = 1.0f, C[NCH] = {0, 0, 0}, S[NCLS] = {0, 0}, weight = 0, D = 0;
                 uint32_t contributor = 0, last_contributor = 0;
+                uint64_t dh = 1469598103934665603ull;  // FNV-1a over the decisions
+                auto mix = [&](uint32_t v) {
+                    for (int b = 0; b < 4; ++b) dh = (dh ^ ((v >> (8 * b)) & 0xffu)) * 1099511628211ull;
+                };
                 for (uint32_t k = r0; k < r1; ++k) {
                     contributor++;
                     const uint32_t g = st->point_list[k];
@@ -474,10 +502,14 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
                     const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
                     const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                     if (power > 0.0f) continue;
-                    const float alpha = std::min(0.99f, co[3] * oracle_exp(power));
+                    const float alpha = std::min(0.99f, co[3] * jitter_exp(oracle_exp(power), g, pix_id));
                     if (alpha < 1.0f / 255.0f) continue;
                     const float test_T = Tr * (1 - alpha);
-                    if (test_T < 0.0001f) break;  // done = true
+                    if (test_T < 0.0001f) {  // done = true
+                        mix(contributor | 0x80000000u);
+                        break;
+                    }
+                    mix(contributor);
                     for (int ch = 0; ch < NCH; ++ch) C[ch] += feat[g * NCH + ch] * alpha * Tr;
                     weight += alpha * Tr;
                     D += st->depths[g] * alpha * Tr;
@@ -486,6 +518,7 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
                     last_contributor = contributor;
                 }
                 st->n_contrib[pix_id] = last_contributor;
+                st->dhash[pix_id] = dh;
                 for (int ch = 0; ch < NCH; ++ch) out_color[(size_t)ch * H * W + pix_id] = C[ch] + Tr * s.bg[ch];
                 out_alpha[pix_id] = weight;
                 st->alpha[pix_id] = weight;
@@ -500,6 +533,15 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
 void oracle_free(void* h) { delete (State*)h; }
 
 int oracle_num_rendered(void* h) { return ((State*)h)->num_rendered; }
+
+// Replace the forward's weight sums (out_alpha, [H*W]) that the backward recovers T_final from
+// (backward.cu:468): lets a study run one backward from another forward's T_final.
+int oracle_set_weight_sums(void* h, const float* alpha) {
+    State* st = (State*)h;
+    if (!alpha) return 1;
+    std::memcpy(st->alpha.data(), alpha, st->alpha.size() * sizeof(float));
+    return 0;
+}
 
 // Copies one named intermediate into dst; returns element count (or -1).
 long oracle_get(void* h, const char* name, void* dst) {
@@ -521,6 +563,7 @@ long oracle_get(void* h, const char* name, void* dst) {
     if (n == "point_list") return cp(st->point_list.data(), st->point_list.size() * 4, st->point_list.size());
     if (n == "ranges") return cp(st->ranges.data(), st->ranges.size() * 4, st->ranges.size());
     if (n == "n_contrib") return cp(st->n_contrib.data(), st->n_contrib.size() * 4, st->n_contrib.size());
+    if (n == "dhash") return cp(st->dhash.data(), st->dhash.size() * 8, st->dhash.size());
     if (n == "gabs") return cp(st->gabs.data(), st->gabs.size() * 4, st->gabs.size());
     g_err = "unknown field " + n;
     return -1;
@@ -582,7 +625,7 @@ int oracle_backward(void* h, const OracleInputs* in, const float* dL_dpix, const
                     const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
                     const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
                     if (power > 0.0f) continue;
-                    const float G = oracle_exp(power);
+                    const float G = jitter_exp(oracle_exp(power), g, pix_id);
                     const float alpha = std::min(0.99f, co[3] * G);
                     if (alpha < 1.0f / 255.0f) continue;
                     Tr = Tr / (1.f - alpha);

@@ -55,6 +55,8 @@ def lib():
         L.oracle_set_num_threads.argtypes = [ctypes.c_int]
         L.oracle_set_acc32.argtypes = [ctypes.c_int]
         L.oracle_set_exp_libm.argtypes = [ctypes.c_int]
+        L.oracle_set_exp_jitter.argtypes = [ctypes.c_uint]
+        L.oracle_set_weight_sums.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_expf.argtypes = [ctypes.c_float]
         L.oracle_expf.restype = ctypes.c_float
         L.oracle_dist_knn3.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p]
@@ -78,7 +80,7 @@ def _ptr(a):
 _FIELD_DTYPES = {
     "depths": np.float32, "means2D": np.float32, "cov3D": np.float32, "conic_opacity": np.float32,
     "rgb": np.float32, "clamped": np.uint8, "tiles_touched": np.uint32, "point_offsets": np.uint32,
-    "keys": np.uint64, "point_list": np.uint32, "ranges": np.uint32, "n_contrib": np.uint32, "gabs": np.float32,
+    "keys": np.uint64, "point_list": np.uint32, "ranges": np.uint32, "n_contrib": np.uint32, "gabs": np.float32, "dhash": np.uint64,
 }
 
 
@@ -91,6 +93,12 @@ def set_acc32(on):
 def set_exp_libm(on):
     """True: blend with the C library's expf instead of gsr_expf (noise-floor studies)."""
     lib().oracle_set_exp_libm(int(bool(on)))
+
+
+def set_exp_jitter(seed):
+    """seed != 0: every blend exp moves by -2 .. +2 ulp (hash of seed, Gaussian, pixel), the
+    same in forward and backward -- the reference algorithm under another faithful exp; 0: off."""
+    lib().oracle_set_exp_jitter(int(seed))
 
 
 def expf(x):
@@ -136,6 +144,13 @@ class OracleRun:
         out = np.zeros((n,), _FIELD_DTYPES[name])
         lib().oracle_get(self.handle, name.encode(), out.ctypes.data)
         return out
+
+    def set_weight_sums(self, alpha):
+        """The backward's T_final = 1 - alpha from another forward (oracle_set_weight_sums)."""
+        a = np.ascontiguousarray(np.asarray(alpha, np.float32).reshape(-1))
+        if a.size != self.W * self.H:
+            raise ValueError("alpha must hold H*W values")
+        lib().oracle_set_weight_sums(self.handle, a.ctypes.data)
 
     def backward(self, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha):
         P, M = self.P, self._settings["M"]

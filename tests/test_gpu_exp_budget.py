@@ -1,81 +1,129 @@
-"""Parity against an INDEPENDENT exp: the HIP path (blending with gsr_expf) vs the CPU
-oracle blending with the C library's expf (glibc, correctly rounded in practice) --
-the closest stand-in here for the reference's CUDA expf (forward.cu:351,
-backward.cu:547; specified at 2 ulp, not reproducible bit for bit off NVIDIA parts).
+"""Parity against an INDEPENDENT exp, stated precisely (VERDICT r4 Next #5).
 
-Two different correctly-rounded-or-nearly exps disagree in the last bit on a small
-fraction of inputs.  The blend thresholds (alpha >= 1/255, T(1-alpha) >= 1e-4) turn a
-last-bit alpha difference into a different decision for a pixel now and then, and the
-backward's T = 1 - sum(alpha T) recovery (backward.cu:468) amplifies it by 1/T_final;
-so some gradient elements move by more than 1e-5 of the tensor maximum ("knife-edge
-outliers") whichever exp either side uses.  The budget below bounds their fraction
-and size per output; it is the DESIGN.md s4 budget, with about 2x headroom over the
-values measured on MI355X (profiles/round2_exp_budget_gsr_expf.jsonl).  The same study
-run with the hardware exp (-DGSR_FAST_EXP: v_exp_f32(x log2e), faithful but not
-correctly rounded; profiles/round2_exp_budget_fast_exp.jsonl) breaks this budget at
-C2 and the metric config (outlier fraction 2x, max 3.5x, image error 300x), which is
-why the kernels keep gsr_expf.
+The HIP path blends with gsr_expf, which the CPU oracle shares bit for bit, so every other
+parity test compares identical exps.  The reference's CUDA expf (forward.cu:351,
+backward.cu:547; specified at 2 ulp) cannot run here; the closest stand-in is the oracle
+blending with the C library's expf (glibc).  Two faithful exps differ in the last bit on a
+fraction of inputs, and that difference reaches the outputs through exactly two mechanisms,
+which this test separates and bounds:
+
+1. Flipped blend decisions.  alpha >= 1/255 and T(1 - alpha) >= 1e-4 (forward.cu:352-359)
+   are thresholds: a last-bit alpha can change which list positions a pixel blends or where it
+   stops.  The oracle hashes every pixel's decision sequence (oracle_get "dhash": the blended
+   positions and the terminating one); pixels whose hash differs between the two exps are
+   the flipped pixels.  They are counted and reported (0 or 1 per view at these configs);
+   everything below is asserted on the other pixels (a flipped pixel's upstream gradients
+   are zeroed, which removes its every gradient term).
+2. The backward's T_final recovery.  backward.cu:468 starts each pixel's back-to-front replay
+   from T_final = 1 - (weight sum) and divides by (1 - alpha) per contributor.  A weight sum
+   that differs in its last bits (|d alpha_out| <= 1e-6 here) becomes a relative error of
+   ~1e-7 / T_final in every T the replay reconstructs; dense scenes have T_final < 1e-3 on
+   most pixels, so 0.1-1 % of gradient elements of the reference itself move by more than
+   1e-5 of the tensor maximum when only the exp changes (measured below, "unpinned").
+   Running the libm backward from the HIP forward's weight sums (oracle set_weight_sums)
+   removes exactly this mechanism.
+
+Asserted per case (c1, sh3, a screen-filling 'large' case, and the BASELINE configs C2, the
+metric scene, C3 and C5 at full size), with G = the oracle with gsr_expf, L = the oracle with
+libm expf run from G's weight sums (mechanism 2 pinned), both on the unflipped pixels:
+  * point_list / num_rendered bit-exact (binning involves no exp);
+  * n_contrib identical on every unflipped pixel; flipped pixels <= 1e-4 of the image;
+  * images within 1e-5 * max(1, |ref|) on unflipped pixels, and the weight sums within 1e-6;
+  * gradients, scale-free (|d| <= tol * max|ref| per element of each tensor, as
+    test_gpu_parity.py), ZERO elements above:
+      (i)   HIP vs G: 1e-5 -- the fp32 summation-order noise test_gpu_parity.py bounds;
+      (ii)  G vs L: 1e-5 -- the exp's direct effect once mechanisms 1 and 2 are removed;
+      (iii) HIP vs L: 2e-5 -- (i) + (ii), so nothing is left unexplained;
+  * the unpinned deviation (L from its own weight sums) is reported per tensor, with a 1e-3
+    regression guard on its maximum.
 """
 import math
 
 import numpy as np
 import pytest
+import torch
 
 import harness as Hn
 from gsr_tools.scene import config_scene_and_camera, synthetic_scene, orbit_camera
 
 pytestmark = pytest.mark.gpu
 
-# case -> (grad outlier fraction, grad max normwise error, image max error, n_contrib mismatch fraction)
-BUDGET = {
-    "c1": (1e-3, 1e-4, 2e-5, 1e-4),
-    "sh3": (1e-3, 1e-4, 2e-5, 1e-4),
-    "large": (0.15, 1e-3, 2e-5, 1e-4),   # 400 screen-filling Gaussians: every pixel sees ~100 of them
-    "c2": (0.05, 5e-4, 2e-5, 1e-4),
-    "mt": (0.02, 5e-4, 2e-5, 1e-4),
-}
+CASES = ["c1", "sh3", "large", "c2", "mt", "c3", "c5"]
+KEYS = ("dmeans2D", "dopacity", "dmeans3D", "dsh", "dscales", "drot", "dsegments")
 
 
 def _case(name):
     if name == "sh3":
         return synthetic_scene(20000, sh_degree=3, seed=3), orbit_camera(1, 333, 250, 300.0)
-    if name == "large":
+    if name == "large":  # 400 screen-filling Gaussians: every pixel sees ~100 of them
         return (synthetic_scene(400, sh_degree=2, seed=9, log_scale=math.log(0.4), log_scale_std=0.3),
                 orbit_camera(3, 300, 200, 250.0))
     return config_scene_and_camera(name)
 
 
-@pytest.mark.parametrize("name", list(BUDGET))
-def test_knife_edge_budget_vs_libm_exp(gpu_available, oracle_mod, name):
-    frac_b, max_b, img_b, nc_b = BUDGET[name]
+def _normwise(a, b, k):
+    a, b = np.asarray(a, np.float64).reshape(b.shape), b.astype(np.float64)
+    if k == "dmeans2D":
+        a, b = a[:, :2], b[:, :2]
+    return np.abs(a - b) / max(float(np.abs(b).max()), 1e-30)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_independent_exp_precise(gpu_available, oracle_mod, name):
+    O = oracle_mod
     scene, cam = _case(name)
-    grads = Hn.upstream_grads(cam.height, cam.width)
-    g = Hn.run_gsr(scene, cam, grads=grads)
-    oracle_mod.set_exp_libm(True)
+    H, W = cam.height, cam.width
+    grads = Hn.upstream_grads(H, W)
+    # decisions under both exps (forward only for gsr_expf: the HIP path's decisions are the
+    # oracle's bit for bit, tests/test_gpu_parity.py)
+    O.set_exp_libm(False)
+    own = O.run_scene(scene, cam)
+    O.set_exp_libm(True)
     try:
-        r = Hn.run_oracle(oracle_mod, scene, cam, grads=grads)
+        lib = O.run_scene(scene, cam)
+        flipped = (own.get("dhash") != lib.get("dhash")).reshape(H, W)
+        keep = ~flipped
+        km = torch.from_numpy(keep)[None]
+        masked = {k: (v * km).contiguous() for k, v in grads.items()}
+        g = Hn.run_gsr(scene, cam, grads=masked)
+        assert g["num_rendered"] == lib.num_rendered
+        np.testing.assert_array_equal(g["point_list"].astype(np.uint32), lib.get("point_list"))
+        nc_lib = lib.get("n_contrib").reshape(H, W)
+        assert np.array_equal(g["n_contrib"].astype(np.uint32)[keep], nc_lib[keep]), "n_contrib on an unflipped pixel"
+        assert flipped.mean() <= 1e-4, f"{int(flipped.sum())} flipped pixels"
+        img = 0.0
+        for k, ref in (("color", lib.color), ("depth", lib.depth), ("alpha", lib.alpha), ("segment", lib.segment)):
+            e = np.abs(g[k].astype(np.float64) - ref) / np.maximum(1.0, np.abs(ref))
+            img = max(img, float(e[:, keep].max()) if keep.any() else 0.0)
+        assert img <= 1e-5, f"image error {img:.2e} on unflipped pixels"
+        dw = float(np.abs(g["alpha"][0].astype(np.float64) - lib.alpha[0])[keep].max()) if keep.any() else 0.0
+        assert dw <= 1e-6, f"weight sums differ by {dw:.2e}"
+        ups = [masked[k].numpy() for k in ("color", "segment", "depth", "alpha")]
+        free = lib.backward(*ups)                # libm backward from its own weight sums
+        lib.set_weight_sums(own.alpha)           # ... and from gsr_expf's (mechanism 2 pinned)
+        pinned = lib.backward(*ups)
     finally:
-        oracle_mod.set_exp_libm(False)
-    # binning does not involve exp: still bit-exact
-    assert g["num_rendered"] == r["num_rendered"]
-    np.testing.assert_array_equal(g["point_list"].astype(np.uint32), r["point_list"])
-    nc = float((g["n_contrib"].astype(np.uint32) != r["n_contrib"]).mean())
-    assert nc <= nc_b, f"n_contrib: {nc:.2e} of pixels differ (budget {nc_b:.0e})"
-    for k in ("color", "depth", "alpha", "segment"):
-        a, b = g[k].astype(np.float64), r[k].astype(np.float64)
-        e = float((np.abs(a - b) / np.maximum(1.0, np.abs(b))).max())
-        assert e <= img_b, f"{k}: max error {e:.2e} (budget {img_b:.0e})"
-    report = {}
-    for k, ref in r["grads"].items():
+        O.set_exp_libm(False)
+    G = own.backward(*ups)
+    del own
+    checks = {"(i) HIP vs G": (g["grads"], G, 1e-5), "(ii) G vs L": (G, pinned, 1e-5),
+              "(iii) HIP vs L": (g["grads"], pinned, 2e-5)}
+    rep, rep_free = {c: {} for c in checks}, {}
+    for k in KEYS:
         if k not in g["grads"]:
             continue
-        a = np.asarray(g["grads"][k], np.float64).reshape(ref.shape)
-        b = ref.astype(np.float64)
-        if k == "dmeans2D":
-            a, b = a[:, :2], b[:, :2]
-        e = np.abs(a - b) / float(np.abs(b).max())
-        frac, mx = float((e > 1e-5).mean()), float(e.max())
-        report[k] = (frac, mx)
-        assert frac <= frac_b, f"{k}: {frac:.2e} of elements above 1e-5 * max|ref| (budget {frac_b:.0e})"
-        assert mx <= max_b, f"{k}: max normwise error {mx:.2e} (budget {max_b:.0e})"
-    print(name, {k: f"frac {f:.1e} max {m:.1e}" for k, (f, m) in report.items()})
+        for c, (x, y, tol) in checks.items():
+            e = _normwise(x[k], y[k], k)
+            rep[c][k] = (int((e > tol).sum()), float(e.max()))
+        f = _normwise(g["grads"][k], free[k], k)
+        rep_free[k] = (float((f > 1e-5).mean()), float(f.max()))
+    print(f"\n{name}: flipped pixels {int(flipped.sum())} of {flipped.size}; image (unflipped) {img:.1e}; "
+          f"|d weight sum| {dw:.1e}")
+    for c, r in rep.items():
+        print(f"  {c:15s} (tol {checks[c][2]:.0e}): " + ", ".join(f"{k} {n} (max {m:.1e})" for k, (n, m) in r.items()))
+    print("  unpinned HIP vs libm: " + ", ".join(f"{k} {fr:.2%} > 1e-5 (max {m:.1e})" for k, (fr, m) in rep_free.items()))
+    for c, r in rep.items():
+        for k, (n, m) in r.items():
+            assert n == 0, f"{c}: {k}: {n} elements above {checks[c][2]:.0e} * max|ref| (max {m:.2e})"
+    for k, (fr, m) in rep_free.items():
+        assert m <= 1e-3, f"{k}: unpinned max normwise deviation {m:.2e}"

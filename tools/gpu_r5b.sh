@@ -1,0 +1,12 @@
+set -o pipefail
+export TMPDIR=/tmp
+mkdir -p gpurun_out/r5b
+timeout -k 10 600 python -u -m pytest tests/test_gpu_exp_budget.py -x -v -s -m gpu --timeout 300 --timeout-method thread > gpurun_out/r5b/exp.log 2>&1 || { tail -40 gpurun_out/r5b/exp.log; exit 1; }
+grep -E "flipped|pinned|unpinned|passed|failed" gpurun_out/r5b/exp.log
+bash tools/ab_kstats.sh 2 > gpurun_out/r5b/ab.log 2>&1 || { tail -20 gpurun_out/r5b/ab.log; exit 1; }
+cat gpurun_out/r5b/ab.log
+timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/r5b/bench.json 2> gpurun_out/r5b/bench.err || { tail -30 gpurun_out/r5b/bench.err; exit 1; }
+python3 -c "
+import json; d=json.load(open('gpurun_out/r5b/bench.json')); r=d['roofline']; b=d['batched']
+print(d['value'], r['avg_launch_ms'], r['avg_launch_ms_timed_region'], r['avg_launch_ms_stage_pass'], r['launches_timed'])
+print(b['value'], b['ratio_to_value'], b['overlap'])"
