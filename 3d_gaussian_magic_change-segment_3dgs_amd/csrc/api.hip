@@ -370,7 +370,7 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
         const bool lb = sort_uses_lookback(P) || sort_grouped_size(P);  // look-back counters to clear
         launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
                           at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect),
-                          packed ? at<uint32_t>(g, L.rect32) : nullptr, at<float>(g, L.shjac),
+                          packed ? at<uint32_t>(g, L.rect32) : nullptr, at<float>(g, L.shjac), at<float>(g, L.opac),
                           g + L.ws, lb ? sort_zero_bytes(P, depth_sort_passes()) : 0,
                           g + L.ws_scan, scan_ws_bytes(P), st);
     }
@@ -635,7 +635,7 @@ int backward_impl(const gsr_settings* s, const gsr_inputs* in, const int* radii,
         gsr_grads gr = *grads;
         if (sh_rows) gr.dsh = nullptr;  // deferred: the exchange writes dsh from the rows
         launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
-                                 at<uint8_t>(g, GL.clamped), contrib, written, at<float4>(g, GL.rec),
+                                 at<uint8_t>(g, GL.clamped), contrib, written, at<float>(g, GL.opac),
                                  at<float>(g, GL.shjac), gr, sh_rows, st);
     }
     GSR_STAGE("gaussian backward");
@@ -774,7 +774,7 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
         w.clamped = at<uint8_t>(g, GL.clamped);
         w.contrib = contrib;
         w.written = written;
-        w.rec = at<float4>(g, GL.rec);
+        w.opac = at<float>(g, GL.opac);
         w.shjac = at<float>(g, GL.shjac);
         w.view = s->viewmatrix;
         w.proj = s->projmatrix;

@@ -132,7 +132,7 @@ size_t rows_bin_ws_bytes(size_t cap);
 // ---- geometry buffer (reference GeometryState, rasterizer_impl.cu:155-171) ----
 struct GeomLayout {
     size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, goff, ws,
-        ws_scan, rect32, rect32_alt, rect32_sorted, shjac, bytes;
+        ws_scan, rect32, rect32_alt, rect32_sorted, shjac, opac, bytes;
 };
 inline GeomLayout geom_layout(size_t P) {
     GeomLayout L{};
@@ -160,6 +160,9 @@ inline GeomLayout geom_layout(size_t P) {
     // d(rgb)/d(dir) of the SH colour, 9 x 64 floats per 64 Gaussians (preprocess writes
     // it, the backward reads it instead of the 192-B SH rows; preprocess.hip sh_dir_jacobian)
     L.shjac = take(cdiv(P, 64) * 64 * 9 * 4);
+    // opacity of each visible Gaussian, for the per-Gaussian backward (which recomputes the
+    // conic and so reads no 64-B record: the record's 32-B half cost a scattered sector read)
+    L.opac = take(P * 4);
     L.bytes = o + ALIGN;
     return L;
 }
@@ -252,7 +255,7 @@ inline char* aligned_base(void* p) {
 // preprocess.hip
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec,
                        int* radii, uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped,
-                       ushort4* rect, uint32_t* rect32, float* shjac, void* zero_a, size_t zero_a_bytes,
+                       ushort4* rect, uint32_t* rect32, float* shjac, float* opac, void* zero_a, size_t zero_a_bytes,
                        void* zero_b, size_t zero_b_bytes, hipStream_t st);
 // the packed rect (GeomLayout::rect32) fits grids of up to 255 x 255 tiles (4080 px)
 inline bool rect_packable(int gx, int gy) { return gx <= 255 && gy <= 255; }
@@ -265,7 +268,7 @@ struct MvView {
     const uint8_t* clamped;
     const float* contrib;
     const uint8_t* written;
-    const float4* rec;
+    const float* opac;   // the view's forward GeomLayout::opac
     const float* shjac;  // the view's SH direction Jacobian (its forward's GeomLayout::shjac)
     const float* view;
     const float* proj;
@@ -290,7 +293,7 @@ void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const 
                         hipStream_t st);
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const uint8_t* written, const float4* rec,
+                              const float* contrib, const uint8_t* written, const float* opac,
                               const float* shjac, const gsr_grads& g, float* shx, hipStream_t st);
 // binning.hip
 // Optional last-pass outputs of a sort: ranges[key] = [first, last + 1) of each key's run in

@@ -339,6 +339,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
                                                     uint32_t* __restrict__ depth_keys,
                                                     uint8_t* __restrict__ clamped, ushort4* __restrict__ rect,
                                                     uint32_t* __restrict__ rect32, float* __restrict__ shjac,
+                                                    float* __restrict__ opac,
                                                     void* zero_a, size_t zero_a16, void* zero_b, size_t zero_b16) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     // clear the depth sort's and the scan's look-back counters (saves two memset launches)
@@ -489,8 +490,13 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     float4* R = rec + (size_t)idx * REC_F4;
     R[0] = make_float4(px, py, conic_x, conic_y);
     R[1] = make_float4(conic_z, opacity, p_view.z, s0);
-    R[2] = make_float4(rgb.x, rgb.y, rgb.z, s1);  // R[3]: padding to 64 B, never read
+    R[2] = make_float4(rgb.x, rgb.y, rgb.z, s1);
+    // R[3] is padding (never read), written anyway: with 48 of the 64 B written, the record's second
+    // 32-B sector was a partial write (read-modify-write in memory).  Measured (rocprof, round 5):
+    // C5 (6M Gaussians) 540 -> 447 us, the metric scene 69.1 -> 68.1 us.
+    R[3] = make_float4(0.f, 0.f, 0.f, 0.f);
     radii[idx] = (int)my_radius;
+    opac[idx] = opacity;
     tiles_touched[idx] = ntiles;
     depth_keys[idx] = __float_as_uint(p_view.z);
     clamped[idx] = cbits;
@@ -600,7 +606,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
                                                            const uint8_t* __restrict__ clamped,
                                                            const float* __restrict__ contrib,
                                                            const uint8_t* __restrict__ written,
-                                                           const float4* __restrict__ rec,
+                                                           const float* __restrict__ opac,
                                                            const float* __restrict__ shjac, gsr_grads g,
                                                            float* __restrict__ shx) {
     // shx != NULL (gsr_backward_deferred_sh): the SH exchange rows of this view -- the
@@ -618,7 +624,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
     load_cam_smem(s, cam);
     const int rad = radii[ci];
     const uint32_t lo_slot = goff[ci], n_slot = tiles_touched[ci];
-    const float4 r0 = rec[(size_t)ci * REC_F4], r1 = rec[(size_t)ci * REC_F4 + 1];
+    const float op = opac[ci];
     const f3 mean = ld3(in.means3D + c3i);
     float c3[6];
     float4 quat = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -670,14 +676,9 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         // [goff, goff + tiles_touched), in slot order (deterministic).
         float q[12];
         sum_records(contrib, written, lo_slot, lo_slot + n_slot, q);
-        const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
-#ifdef GSR_MOMENT_MEAN
-        const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * s.W);
-        const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * s.H);
-#else
+        // the conic weighting of the mean2D channels happened per lane in the render backward
         const float dm2x = -op * q[7] * (0.5f * s.W);  // q[7] = sum q (a dx + b dy)
         const float dm2y = -op * q[8] * (0.5f * s.H);  // q[8] = sum q (b dx + c dy)
-#endif
         if (g.dmeans2D) { g.dmeans2D[i3] = dm2x; g.dmeans2D[i3 + 1] = dm2y; g.dmeans2D[i3 + 2] = 0.f; }
         if (g.dcolors) { g.dcolors[i3] = q[0]; g.dcolors[i3 + 1] = q[1]; g.dcolors[i3 + 2] = q[2]; }
         if (g.dopacity) g.dopacity[idx] = q[6];
@@ -945,17 +946,11 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int D, int 
             if (drgb_v) { drgb_v[0] = 0.f; drgb_v[1] = 0.f; drgb_v[2] = 0.f; }
             continue;
         }
-        const float4 r0 = w.rec[(size_t)idx * REC_F4], r1 = w.rec[(size_t)idx * REC_F4 + 1];
+        const float op = w.opac[idx];
         float q[12];
         sum_records(w.contrib, w.written, w.goff[idx], w.goff[idx] + w.tiles_touched[idx], q);
-        const float ca = r0.z, cb = r0.w, cc = r1.x, op = r1.y;
-#ifdef GSR_MOMENT_MEAN
-        const float dm2x = -op * (ca * q[7] + cb * q[8]) * (0.5f * w.W);
-        const float dm2y = -op * (cc * q[8] + cb * q[7]) * (0.5f * w.H);
-#else
         const float dm2x = -op * q[7] * (0.5f * w.W);  // q[7] = sum q (a dx + b dy)
         const float dm2y = -op * q[8] * (0.5f * w.H);  // q[8] = sum q (b dx + c dy)
-#endif
         if (w.dmeans2D) { w.dmeans2D[i3] = dm2x; w.dmeans2D[i3 + 1] = dm2y; w.dmeans2D[i3 + 2] = 0.f; }
         dcol = dcol + f3{q[0], q[1], q[2]};
         dop += q[6];
@@ -1191,11 +1186,11 @@ __global__ void __launch_bounds__(256) k_sh_dsh(int P, int D, int M, const float
 #if GSR_PRE_PART == 1
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec, int* radii,
                        uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped, ushort4* rect,
-                       uint32_t* rect32, float* shjac, void* zero_a, size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes,
-                       hipStream_t st) {
+                       uint32_t* rect32, float* shjac, float* opac, void* zero_a, size_t zero_a_bytes, void* zero_b,
+                       size_t zero_b_bytes, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_preprocess, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, gx, gy, rec, radii,
-                       tiles_touched, depth_keys, clamped, rect, rect32, shjac, zero_a, cdiv(zero_a_bytes, 16), zero_b,
+                       tiles_touched, depth_keys, clamped, rect, rect32, shjac, opac, zero_a, cdiv(zero_a_bytes, 16), zero_b,
                        cdiv(zero_b_bytes, 16));
 }
 
@@ -1229,11 +1224,11 @@ void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const 
 #if GSR_PRE_PART == 2
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
                               const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const uint8_t* written, const float4* rec,
+                              const float* contrib, const uint8_t* written, const float* opac,
                               const float* shjac, const gsr_grads& g, float* shx, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_gaussian_backward, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, radii, tiles_touched,
-                       goff, clamped, contrib, written, rec, shjac, g, in.shs ? shx : nullptr);
+                       goff, clamped, contrib, written, opac, shjac, g, in.shs ? shx : nullptr);
 }
 
 #endif  // GSR_PRE_PART == 2

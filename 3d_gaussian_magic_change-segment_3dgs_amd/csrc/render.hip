@@ -30,9 +30,8 @@
 // d = (dx, dy) = mean2D - pixel, conic (a, b, c)), 12 floats:
 //   [0..5]  sum dch*dL_dcolor.rgb, sum dch*dL_dseg0/1, sum dch*dL_ddepth
 //   [6]     sum q
-//   [7] [8] default: sum q (a dx + b dy), sum q (b dx + c dy)   (the reference's dG_ddelx /
-//           dG_ddely weighting, backward.cu:612-621, formed per lane before the reduction)
-//           GSR_MOMENT_MEAN builds: sum q dx, sum q dy
+//   [7] [8] sum q (a dx + b dy), sum q (b dx + c dy)   (the reference's dG_ddelx / dG_ddely
+//           weighting, backward.cu:612-621, formed per lane before the reduction)
 //   [9..11] sum q dx^2, sum q dx dy, sum q dy^2
 // from which k_gaussian_backward (preprocess.hip) forms dopacity = sum q and the reference's
 // mean2D / conic gradients with the Gaussian's own conic and opacity.
@@ -365,10 +364,6 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
     }
     const uint2 range = ranges[tile];
     const int n = (int)(range.y - range.x);
-#ifdef GSR_FWD_CK_BY_N
-    // a tile shorter than ck + CK_MIN_BACK is never split (publish_depth): no checkpoint
-    if (n < ck + (int)CK_MIN_BACK) ck = 0;
-#endif
     STAT_DECL
     STAT(7, n);
     // prefilter rectangle: the pixels this wave owns
@@ -910,9 +905,6 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                 todo &= todo - 1;
                 const uint32_t p = (uint32_t)(top - 1 - j);
                 const float4 q0 = srec[j][0], q1 = srec[j][1];
-#ifdef GSR_BWD_EARLY_REC
-                const float4 q2 = srec[j][2], q3 = srec[j][3];  // one LDS wait per instance
-#endif
                 const float gx_ = q0.x, gy_ = q0.y, ca = q0.z, cb = q0.w, cc = q1.x, pm = q1.y;
                 float power[NS], dys[NS];
                 uint64_t act[NS];
@@ -951,9 +943,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                     continue;
                 }
                 STAT(3, 1);
-#ifndef GSR_BWD_EARLY_REC
                 const float4 q2 = srec[j][2], q3 = srec[j][3];
-#endif
                 const float op = q1.z, dep = q3.x, s0v = q1.w;
 #ifdef GSR_STATS
                 unsigned long long okst_ = st_[12];
@@ -1013,11 +1003,6 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                     Dk[k] = __builtin_fmaf(a_m, diff, Dk[k]);
                     T[k] = Tn;
                 }
-#ifdef GSR_MOMENT_MEAN
-                acc[7] = dx * acc[6];   // sum q dx   (dx is shared by the lane's pixels)
-                acc[9] = dx * acc[7];   // sum q dx^2
-                acc[10] = dx * acc[8];  // sum q dx dy
-#else
                 // The mean2D channels carry the conic-weighted sums per lane,
                 // sum q (a dx + b dy) and sum q (b dx + c dy), as the reference's per-pixel
                 // dG_ddelx / dG_ddely terms (backward.cu:612-621), instead of the moments
@@ -1031,7 +1016,6 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
                     acc[7] = __builtin_fmaf(ca, qx, cb * qy);
                     acc[8] = __builtin_fmaf(cc, qy, cb * qx);
                 }
-#endif
 #ifdef GSR_STATS
                 STAT(11, st_[12] == okst_);
 #endif

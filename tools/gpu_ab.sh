@@ -1,14 +1,19 @@
 #!/bin/bash
-# gpu_ab.sh: GPU tests, then the default build against build/variants/libgsr_*.so twice
-# (render and binning stages), then a kernel-trace timeline of the default build.
+# GPU session: the -m gpu suite, then a rocprof A/B of the default build against every
+# build/variants/libgsr_*.so (tools/ab_kstats.sh; metric scene, ROUNDS rounds; optionally C5).
+# Usage: tools/gpu_ab.sh TAG [ROUNDS] [c5]
 set -o pipefail
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > gpurun_out/ab_tests.log 2>&1 || { tail -30 gpurun_out/ab_tests.log; exit 1; }
-tail -1 gpurun_out/ab_tests.log
-bash tools/bench_stage_variants.sh ${AB_STAGES:-render_bwd render_fwd depth_sort} || exit 1
-bash tools/bench_stage_variants.sh ${AB_STAGES:-render_bwd render_fwd depth_sort} || exit 1
-rm -rf gpurun_out/ab_prof
-timeout -k 10 200 rocprofv3 --kernel-trace -d gpurun_out/ab_prof -o kt --output-format csv -- python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-train --batched-views 1 > gpurun_out/ab_prof.log 2>&1 || { tail -20 gpurun_out/ab_prof.log; exit 1; }
-python tools/timeline.py "$(find gpurun_out/ab_prof -name "*kernel_trace.csv" -print -quit)" > gpurun_out/ab_timeline.txt && sed -n 1,8p gpurun_out/ab_timeline.txt
+T=${1:-ab}; R=${2:-2}
+O=gpurun_out/$T
+mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -x -v -m gpu --timeout 200 --timeout-method thread > $O/pytest_gpu.log 2>&1 \
+  || { tail -40 $O/pytest_gpu.log; exit 1; }
+tail -2 $O/pytest_gpu.log
+bash tools/ab_kstats.sh $R > $O/ab.log 2>&1 || { tail -20 $O/ab.log; exit 1; }
+cat $O/ab.log
+if [ "$3" = "c5" ]; then
+  CONFIG=c5 AB_STEPS=12 bash tools/ab_kstats.sh 1 > $O/ab_c5.log 2>&1 || { tail -20 $O/ab_c5.log; exit 1; }
+  cat $O/ab_c5.log
+fi
