@@ -189,7 +189,10 @@ inline BinLayout bin_layout(size_t I) {
 }
 
 // ---- backward scratch: per-instance gradient records ----
-inline size_t scratch_bytes(size_t I) { return align_up(I * 12 * sizeof(float)) + ALIGN; }
+// Backward scratch: one 48-B gradient record per instance slot.  (64-B records, whole 32-B sectors
+// per record, measured slower: the per-Gaussian gather touches more lines, round 5.)
+constexpr int CONTRIB_STRIDE = 12;
+inline size_t scratch_bytes(size_t I) { return align_up(I * CONTRIB_STRIDE * sizeof(float)) + ALIGN; }
 
 // ---- image buffer (reference ImageState, rasterizer_impl.cu:173-179) ----
 // After the T entries of the tile order (img buffer), the render schedule:

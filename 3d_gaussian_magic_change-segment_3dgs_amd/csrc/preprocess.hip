@@ -550,7 +550,7 @@ __device__ __forceinline__ void sum_records(const float* __restrict__ contrib, c
             float4 r[4][3];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
-                const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)u[k] * 12);
+                const float4* src = reinterpret_cast<const float4*>(contrib + (size_t)u[k] * CONTRIB_STRIDE);
                 if (k == 0 || v[k]) {
                     r[k][0] = src[0]; r[k][1] = src[1]; r[k][2] = src[2];
                 } else {

@@ -844,7 +844,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
     auto flush = [&]() {
         if constexpr (!SPLIT) {
             if ((prev_touched >> lane) & 1ull) {
-                float4* d = reinterpret_cast<float4*>(contrib + (size_t)prev_uslot * 12);
+                float4* d = reinterpret_cast<float4*>(contrib + (size_t)prev_uslot * CONTRIB_STRIDE);
                 const float4 a = stage[lane][0], b = stage[lane][1], c = stage[lane][2];
                 d[0] = a;
                 d[1] = b;
@@ -1047,7 +1047,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
 #pragma unroll
                     for (int c = 0; c < 6; ++c)
                         v[c] = (w0 ? sh->part[0][jj][6 * h + c] : 0.f) + (w1 ? sh->part[1][jj][6 * h + c] : 0.f);
-                    float2* d = reinterpret_cast<float2*>(contrib + (size_t)u * 12 + 6 * h);
+                    float2* d = reinterpret_cast<float2*>(contrib + (size_t)u * CONTRIB_STRIDE + 6 * h);
                     d[0] = make_float2(v[0], v[1]);
                     d[1] = make_float2(v[2], v[3]);
                     d[2] = make_float2(v[4], v[5]);
