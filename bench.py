@@ -623,12 +623,14 @@ def main():
         # for point-to-point xGMI; SURVEY.md s8e / DESIGN.md s7).
         bstep = make_step(BB)
         # its own warm-up: the first batched steps grow the caching allocator's pools on both
-        # streams (BENCH_r04 timed 8 steps after 1 warm-up step: 1.014x; 25 after 2: 1.055x)
-        for _ in range(max(3, args.warmup // 4)):
+        # streams and refill the binning-capacity guesses (BENCH_r04 timed 8 steps after 1
+        # warm-up step: 1.014x; 16 after 3: 1.02x; the batched mode as the main measurement, 40
+        # steps after 8: 1.062x, profiles/round5_bprof_kernel_stats.csv)
+        for _ in range(max(8, args.warmup // 2)):
             bstep()
         drain()
         torch.cuda.synchronize()
-        k = max(16, args.steps // BB)
+        k = max(32, args.steps // BB)
         el_b = timed(bstep, k)
         # overlap of the two streams: every stage bracketed (untimed, 3 steps) -> the stage busy
         # time summed over both streams per step, against the wall time of the same steps
