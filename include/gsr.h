@@ -114,6 +114,11 @@ GSR_API size_t gsr_binning_bytes(int num_rendered);
 /* largest C with gsr_binning_bytes(C) <= bytes (-1 if none): the layout capacity of a binning
  * buffer of that size (settings.binning_capacity) */
 GSR_API int gsr_binning_capacity(size_t bytes);
+/* image-state buffer of a W x H view (ImageState, rasterizer_impl.cu:173-179).  Besides the
+ * reference's ranges and n_contrib it holds the heavy-first tile schedule and, per 16x16 tile,
+ * the forward's list-segment checkpoint for the backward (9 floats per pixel, 36 B): about
+ * 88 MB in all at 1920 x 1080, 349 MB at 3840 x 2160, allocated whether or not a tile is deep enough
+ * to use it; a multi-view forward keeps one per view until its backward. */
 GSR_API size_t gsr_img_bytes(int W, int H);
 /* scratch needed by gsr_backward (per-instance gradient records) */
 GSR_API size_t gsr_backward_scratch_bytes(int num_rendered);
