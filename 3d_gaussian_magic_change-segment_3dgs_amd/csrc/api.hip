@@ -466,9 +466,8 @@ int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* b
             auto rb = [&](int stage) {
                 launch_rows_binning(P, IL.gx, IL.gy, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets),
                                     at<uint32_t>(g, GL.rect32_sorted), at<uint32_t>(g, GL.goff), g + GL.ws, b + BL.ws,
-                                    at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.tkeys_alt),
-                                    at<uint32_t>(b, BL.vals_alt), at<uint32_t>(b, BL.point_list),
-                                    at<uint32_t>(b, BL.slot_vals), ranges, order, at<uint4>(b, BL.written),
+                                    at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.vals_alt),
+                                    at<uint32_t>(b, BL.point_list), ranges, order, at<uint4>(b, BL.written),
                                     cdiv(cap, 16), cap, n_total, st, stage, /*fused=*/true,
                                     n_dev && !t_tallied ? host_total_slot().dev : nullptr);
             };
@@ -624,7 +623,7 @@ int backward_impl(const gsr_settings* s, const gsr_inputs* in, const int* radii,
             StageScope sc(GSR_STAGE_RENDER_BWD, st);
             launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order),
                                    at<uint32_t>(im, IL.order) + IL.gx * IL.gy, at<uint2>(im, IL.ranges),
-                                   at<uint32_t>(b, BL.point_list), at<uint32_t>(b, BL.slot_vals),
+                                   at<uint32_t>(b, BL.point_list), at<uint32_t>(g, GL.goff),
                                    at<float4>(g, GL.rec), s->bg, alpha, at<uint32_t>(im, IL.n_contrib), dL_dcolor,
                                    dL_dsegment, dL_ddepth, dL_dalpha, contrib, written, at<float>(im, IL.ckpt), st);
         }
@@ -755,7 +754,7 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
                 launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order),
                                        at<uint32_t>(im, IL.order) + IL.gx * IL.gy, at<uint2>(im, IL.ranges),
                                        at<uint32_t>(b, BL.point_list),
-                                       at<uint32_t>(b, BL.slot_vals), at<float4>(g, GL.rec), s->bg, V.alpha,
+                                       at<uint32_t>(g, GL.goff), at<float4>(g, GL.rec), s->bg, V.alpha,
                                        at<uint32_t>(im, IL.n_contrib), V.dL_dcolor, V.dL_dsegment, V.dL_ddepth,
                                        V.dL_dalpha, contrib, written, at<float>(im, IL.ckpt), sv);
             }

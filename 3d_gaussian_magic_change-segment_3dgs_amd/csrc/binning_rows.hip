@@ -195,8 +195,9 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_count(int P, int gy, int nch1, 
     zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH1 + threadIdx.x, (size_t)gridDim.x * RB_CH1);
 }
 
-// Level-1 entries (E1, grouped by row): e_gid = Gaussian id, e_u = its first instance slot
-// in the row, e_x = x0 | x1 << 8.  Also goff[gid] (the backward's record slots).
+// Level-1 entries (E1, grouped by row): e_gid = Gaussian id, e_x = x0 | x1 << 8.  Also goff[gid],
+// the Gaussian's first record slot (its instance (x, y) has slot goff + (y - y0) w + (x - x0): the
+// render backward forms it from goff and the rectangle in the Gaussian's record).
 // Dynamic LDS: bits + pre, 2 x gy x RB_S1 words, sized by the grid rather than the 255
 // bound (gy = 68 at 1080p: 18 KB; 67 KB at gy = 255, covered by the 4080-px-tall case of
 // tests/test_gpu_parity.py::test_rows_binning_matches_radix_path).  Every global load is
@@ -210,14 +211,14 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_scatter(int P, int gy, int nch1
                                                         uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ rect,
                                                         const uint32_t* __restrict__ base1, uint32_t* __restrict__ goff,
-                                                        uint32_t* __restrict__ e_gid, uint32_t* __restrict__ e_u,
+                                                        uint32_t* __restrict__ e_gid,
                                                         uint32_t* __restrict__ e_x, uint32_t cap, int fused,
                                                         uint32_t* host_total) {
     extern __shared__ uint32_t dyn[];
     uint32_t* bits = dyn;
     uint32_t* pre = dyn + gy * RB_S1;
     __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
-    __shared__ uint32_t s_gid[RB_STAGE1], s_u[RB_STAGE1], s_x[RB_STAGE1];
+    __shared__ uint32_t s_gid[RB_STAGE1], s_x[RB_STAGE1];
     __shared__ uint32_t tot;
     __shared__ uint32_t s_wsum[RB_CH1 / 64];
     BT_T(bt0)
@@ -260,21 +261,18 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_scatter(int P, int gy, int nch1
     const bool staged = tot <= (uint32_t)RB_STAGE1;  // uniform
     if (vis) {
         goff[g] = off;
-        const uint32_t w = (uint32_t)(x1 - x0), below = bit - 1u;
+        const uint32_t below = bit - 1u;
         for (int y = y0; y < y1; ++y) {
             const uint32_t rank = pre[y * RB_S1 + wd] + (uint32_t)__popc(bits[y * RB_S1 + wd] & below);
-            const uint32_t u = off + (uint32_t)(y - y0) * w;
             const uint32_t xr = (uint32_t)x0 | ((uint32_t)x1 << 8) | ((uint32_t)y << 16);
             if (staged) {
                 const uint32_t lp = lst[y] + rank;
                 s_gid[lp] = g;
-                s_u[lp] = u;
                 s_x[lp] = xr;
             } else {
                 const uint32_t gp = gb[y] + rank;
                 if (gp < cap) {
                     e_gid[gp] = g;
-                    e_u[gp] = u;
                     e_x[gp] = xr & 0xFFFFu;
                 }
             }
@@ -287,7 +285,6 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_scatter(int P, int gy, int nch1
         const uint32_t gp = gb[y] + (i - lst[y]);
         if (gp < cap) {
             e_gid[gp] = s_gid[i];
-            e_u[gp] = s_u[i];
             e_x[gp] = xr & 0xFFFFu;
         }
     }
@@ -402,7 +399,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_count(int gx, int gy, int nch1,
     (void)nch_;
 }
 
-// point_list / slot_vals; the ranges of every non-empty row (from the chunk s = 0 of the
+// point_list; the ranges of every non-empty row (from the chunk s = 0 of the
 // row: the first entry of (y, x, 0) and of the next column, clamped to the capacity, empty
 // tiles {0, 0}); also clears the backward's written-slot flags.  The next chunk's entries
 // and bucket bases are loaded while the current one is ranked (software pipeline: a chunk
@@ -412,10 +409,8 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
                                                          const uint32_t* __restrict__ base1,
                                                          const uint32_t* __restrict__ base2,
                                                          const uint32_t* __restrict__ e_gid,
-                                                         const uint32_t* __restrict__ e_u,
                                                          const uint32_t* __restrict__ e_x,
-                                                         uint32_t* __restrict__ point_list,
-                                                         uint32_t* __restrict__ slot_vals, uint32_t cap,
+                                                         uint32_t* __restrict__ point_list, uint32_t cap,
                                                          const uint32_t* __restrict__ n_total,
                                                          uint2* __restrict__ ranges, uint4* zero, size_t nzero16,
                                                          uint32_t* __restrict__ bucket_words) {
@@ -424,7 +419,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
     uint32_t* pre = dyn + gx * RB_S;
     __shared__ RowMap m;
     __shared__ uint32_t cnt[RB_MAXB], lst[RB_MAXB], gb[RB_MAXB];
-    __shared__ uint32_t s_gid[RB_STAGE], s_u[RB_STAGE], s_gp[RB_STAGE];
+    __shared__ uint32_t s_gid[RB_STAGE], s_gp[RB_STAGE];
     __shared__ uint32_t tot;
     __shared__ uint32_t s_bc[FINE_BUCKETS];  // this row's tiles per fine schedule bucket (k_tile_order_counted)
     BT_T(bt0)
@@ -437,7 +432,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
     // chunk c -> its row, sub-chunk, entries, this thread's entry and bucket base (prefetch)
     struct Chunk {
         int y;
-        uint32_t s, e0, n, g, u, xr, gbv;
+        uint32_t s, e0, n, g, xr, gbv;
     };
     auto fetch = [&](uint32_t c) {
         Chunk k;
@@ -445,10 +440,9 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
         k.s = c - m.c0[k.y];
         k.e0 = m.rs[k.y] + k.s * RB_CH;
         k.n = min((uint32_t)RB_CH, m.rs[k.y + 1] - k.e0);
-        k.g = k.u = k.xr = 0;
+        k.g = k.xr = 0;
         if ((uint32_t)tid < k.n) {
             k.g = e_gid[k.e0 + tid];
-            k.u = e_u[k.e0 + tid];
             k.xr = e_x[k.e0 + tid];
         }
         k.gbv = tid < gx ? base2[tile_slot(m, gx, k.y, tid, k.s)] : 0u;
@@ -493,33 +487,25 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
         if (live)
             for (int x = x0; x < x1; ++x) {
                 const uint32_t rank = pre[x * RB_S + wd] + (uint32_t)__popc(bits[x * RB_S + wd] & below);
-                const uint32_t uu = cur.u + (uint32_t)(x - x0);
                 if (staged) {
                     const uint32_t lp = lst[x] + rank;
                     s_gid[lp] = cur.g;
-                    s_u[lp] = uu;
                     s_gp[lp] = gb[x] + rank;
                 } else {
                     const uint32_t gp = gb[x] + rank;
-                    if (gp < cap) {
-                        point_list[gp] = cur.g;
-                        slot_vals[gp] = uu;
-                    }
+                    if (gp < cap) point_list[gp] = cur.g;
                 }
             }
         // The next chunk's prefetched values are waited for here, before this chunk's output
         // stores: gfx950 counts loads and stores in one in-order vmcnt, so a first use after
         // a store loop of unknown length becomes vmcnt(0) -- a wait for every store's
         // acknowledgement once per chunk.
-        asm volatile("" ::"v"(nxt.g), "v"(nxt.u), "v"(nxt.xr), "v"(nxt.gbv));
+        asm volatile("" ::"v"(nxt.g), "v"(nxt.xr), "v"(nxt.gbv));
         if (staged) {
             __syncthreads();
             for (uint32_t i = tid; i < tot; i += RB_CH) {
                 const uint32_t gp = s_gp[i];
-                if (gp < cap) {
-                    point_list[gp] = s_gid[i];
-                    slot_vals[gp] = s_u[i];
-                }
+                if (gp < cap) point_list[gp] = s_gid[i];
             }
         } else {
             __syncthreads();  // gb and bits are rewritten at the top of the next chunk
@@ -550,8 +536,8 @@ size_t rows_bin_ws_bytes(size_t cap) {
 }
 
 void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, uint32_t* offsets, const uint32_t* rect,
-                         uint32_t* goff, void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_u, uint32_t* e_x,
-                         uint32_t* point_list, uint32_t* slot_vals, uint2* ranges, uint32_t* tile_order,
+                         uint32_t* goff, void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_x,
+                         uint32_t* point_list, uint2* ranges, uint32_t* tile_order,
                          uint4* written, size_t written16, size_t cap, const uint32_t* n_total, hipStream_t st,
                          int stage, bool fused, uint32_t* host_total) {
     const int nch1 = (int)cdiv(P, RB_CH1);
@@ -577,14 +563,14 @@ void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, uint32_t*
                            cdiv(S1.bytes, 16), (int)fused);
         launch_scan_exclusive(table1, base1, n1, nullptr, S1, st);
         hipLaunchKernelGGL(k_rows_scatter, dim3(nch1), dim3(RB_CH1), 2 * gy * RB_S1 * 4, st, P, gy, nch1, order,
-                           offsets, rect, base1, goff, e_gid, e_u, e_x, cap32, (int)fused, host_total);
+                           offsets, rect, base1, goff, e_gid, e_x, cap32, (int)fused, host_total);
     } else if (stage == 1) {  // level 2: tiles (+ ranges)
         const int grid2 = (int)std::min<size_t>(RB_GRID2, gy + cdiv(cap, RB_CH));
         hipLaunchKernelGGL(k_tiles_count, dim3(grid2), dim3(RB_CH), 0, st, gx, gy, nch1, table1, base1, e_x, table2,
                            len2, cap32, S2.base, cdiv(S2.bytes, 16), ranges, bucket_words);
         launch_scan_exclusive(table2, base2, n2, len2, S2, st);
         hipLaunchKernelGGL(k_tiles_scatter, dim3(grid2), dim3(RB_CH), 2 * gx * RB_S * 4, st, gx, gy, nch1, table1,
-                           base1, base2, e_gid, e_u, e_x, point_list, slot_vals, cap32, n_total, ranges, written,
+                           base1, base2, e_gid, e_x, point_list, cap32, n_total, ranges, written,
                            written16, bucket_words);
     } else {  // heavy-first tile order from the bucket counts (binning.hip)
         launch_tile_order_counted(ranges, gx * gy, bucket_words, tile_order, st);

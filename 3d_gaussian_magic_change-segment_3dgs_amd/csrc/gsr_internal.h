@@ -354,15 +354,15 @@ void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_id
 void launch_scan_exclusive(const uint32_t* src, uint32_t* out, size_t n, const uint32_t* n_dev, const ScanWs& W,
                            hipStream_t st);
 // binning_rows.hip: tile lists by row-then-tile expansion (grids up to 255 x 255 tiles).
-// stage 0: level 1 (rows, goff); 1: level 2 (point_list, slot_vals, written flags
+// stage 0: level 1 (rows, goff); 1: level 2 (point_list, written flags
 // cleared); 2: ranges + heavy-first tile order.  geom_ws: rows_bin_geom_ws_bytes(P, gy)
 // bytes (the depth sort's workspace, free by then); bin_ws: rows_bin_ws_bytes(cap).
 // fused: level 1 also computes the depth-ordered instance offsets (written to offsets, as the
 // depth-order scan writes them; num_rendered also to host_total when non-NULL), so the scan need
 // not run first.
 void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, uint32_t* offsets, const uint32_t* rect,
-                         uint32_t* goff, void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_u, uint32_t* e_x,
-                         uint32_t* point_list, uint32_t* slot_vals, uint2* ranges, uint32_t* tile_order,
+                         uint32_t* goff, void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_x,
+                         uint32_t* point_list, uint2* ranges, uint32_t* tile_order,
                          uint4* written, size_t written16, size_t cap, const uint32_t* n_total, hipStream_t st,
                          int stage, bool fused, uint32_t* host_total);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
@@ -377,7 +377,7 @@ void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, 
                            float* out_color, float* out_depth, float* out_alpha, float* out_segment,
                            uint32_t* n_contrib, float* ckpt, hipStream_t st);
 void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
-                            const uint2* ranges, const uint32_t* point_list, const uint32_t* slot_vals,
+                            const uint2* ranges, const uint32_t* point_list, const uint32_t* goff,
                             const float4* rec, const float* bg, const float* alpha, const uint32_t* n_contrib,
                             const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
                             const float* dL_dalpha, float* contrib, uint8_t* written, const float* ckpt,

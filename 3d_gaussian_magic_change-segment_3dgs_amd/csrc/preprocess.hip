@@ -491,10 +491,13 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     R[0] = make_float4(px, py, conic_x, conic_y);
     R[1] = make_float4(conic_z, opacity, p_view.z, s0);
     R[2] = make_float4(rgb.x, rgb.y, rgb.z, s1);
-    // R[3] is padding (never read), written anyway: with 48 of the 64 B written, the record's second
-    // 32-B sector was a partial write (read-modify-write in memory).  Measured (rocprof, round 5):
-    // C5 (6M Gaussians) 540 -> 447 us, the metric scene 69.1 -> 68.1 us.
-    R[3] = make_float4(0.f, 0.f, 0.f, 0.f);
+    // R[3]: the tile rectangle (x0 | y0 << 16, x1 | y1 << 16), from which the render backward forms
+    // an instance's record slot goff + (y - y0) (x1 - x0) + (x - x0) (binning_rows.hip) -- so the
+    // binning writes no per-instance slot array.  All 64 B are written: with 48 written, the
+    // record's second 32-B sector was a partial write (read-modify-write in memory; rocprof, round
+    // 5: C5 preprocess 540 -> 447 us, the metric scene 69.1 -> 68.1 us).
+    R[3] = make_float4(__uint_as_float((uint32_t)x0 | ((uint32_t)y0 << 16)),
+                       __uint_as_float((uint32_t)x1 | ((uint32_t)y1 << 16)), 0.f, 0.f);
     radii[idx] = (int)my_radius;
     opac[idx] = opacity;
     tiles_touched[idx] = ntiles;

@@ -215,6 +215,23 @@ __device__ __forceinline__ Batch fetch_batch(const float4* __restrict__ rec, uin
     const float4* R = rec + (size_t)g * REC_F4;
     return Batch{R[0], R[1], R[2]};
 }
+// The backward's batch fetch also takes the Gaussian's tile rectangle (record part 3, in the
+// 32-B sector of part 2) and its first record slot goff: the instance's slot is then
+// goff + (ty - y0) (x1 - x0) + (tx - x0) -- no per-instance slot array to read.
+struct BatchB {
+    float4 a, b, c;
+    uint2 r;
+    uint32_t go;
+};
+__device__ __forceinline__ BatchB fetch_batch_b(const float4* __restrict__ rec, const uint32_t* __restrict__ goff,
+                                                uint32_t g) {
+    const float4* R = rec + (size_t)g * REC_F4;
+    return BatchB{R[0], R[1], R[2], *reinterpret_cast<const uint2*>(R + 3), goff[g]};
+}
+__device__ __forceinline__ uint32_t batch_slot(const BatchB& b, int tx, int ty) {
+    const uint32_t x0 = b.r.x & 0xFFFFu, y0 = b.r.x >> 16, x1 = b.r.y & 0xFFFFu;
+    return b.go + ((uint32_t)ty - y0) * (x1 - x0) + ((uint32_t)tx - x0);
+}
 
 // Lane-parallel batch prefilter: can ANY pixel centre of the tile rectangle
 // [x0,x1] x [y0,y1] reach power >= pm for the Gaussian (x, y, conic a, b, c)?
@@ -719,7 +736,7 @@ template <int NS, bool SPLIT>
 __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0, int wslot,
                                          const uint2* __restrict__ ranges,
                                          const uint32_t* __restrict__ point_list,
-                                         const uint32_t* __restrict__ slot_vals,
+                                         const uint32_t* __restrict__ goff,
                                          const float4* __restrict__ rec, const float* __restrict__ bg,
                                          const float* __restrict__ alphas,
                                          const uint32_t* __restrict__ n_contrib,
@@ -820,20 +837,14 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
     // Same two-stage batch pipeline and LDS record broadcast as the forward, walking
     // the list back to front: lane l of the batch with upper end `top` owns position top-1-l.
     const uint32_t* plist = point_list + range.x;
-    const uint32_t* slist = slot_vals + range.x;
     // list positions below 0 are clamped to 0 (unconditional loads, see fetch_batch)
-    uint32_t g_next = 0u, u_next = 0u;
-    Batch cur;
+    uint32_t g_next = 0u;
+    BatchB cur;
     if (top0 > 0) {
         g_next = plist[max(top0 - 1 - lane, 0)];
-        u_next = slist[max(top0 - 1 - lane, 0)];
-        cur = fetch_batch(rec, g_next);
+        cur = fetch_batch_b(rec, goff, g_next);
     }
-    uint32_t u_cur = u_next;
-    if (top0 > 0) {
-        g_next = plist[max(top0 - 65 - lane, 0)];
-        u_next = slist[max(top0 - 65 - lane, 0)];
-    }
+    if (top0 > 0) g_next = plist[max(top0 - 65 - lane, 0)];
     // Unsplit tiles park a batch's records in LDS (stage[j] = record of batch instance j) and
     // store them at the start of the next batch, ahead of its prefetch loads.  gfx950 counts
     // vector loads and stores in one in-order vmcnt: with the records stored inside the batch,
@@ -859,14 +870,11 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
             const int cnt = min(64, top - seg_lo);
             STAT(5, 1);
             flush();
-            const Batch nxt = fetch_batch(rec, g_next);
-            const uint32_t u_nxt = u_next;
+            const BatchB nxt = fetch_batch_b(rec, goff, g_next);
             g_next = plist[max(top - 129 - lane, 0)];
-            u_next = slist[max(top - 129 - lane, 0)];
             const float4 ra = cur.a, rb = cur.b, rc = cur.c;
-            const uint32_t uslot = u_cur;
+            const uint32_t uslot = batch_slot(cur, tx, ty);  // the instance's record slot
             cur = nxt;
-            u_cur = u_nxt;
             const float pmin = power_floor(rb.y);
             // Lanes replaying every position of this batch (p < n_contrib for all p < top) and
             // whether any lane starts replaying inside it: only then is p < n_contrib
@@ -1084,7 +1092,7 @@ __device__ __forceinline__ uint32_t queue_tile(const TileSched& ts, int T, uint3
 
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k_render_bwd(
     int W, int H, int gx, int T, int split_depth, uint32_t* __restrict__ sched,
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ slot_vals,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ goff,
     const float4* __restrict__ rec, const float* __restrict__ bg, const float* __restrict__ alphas,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ dL_dsegs,
     const float* __restrict__ dL_ddepths, const float* __restrict__ dL_dalphas, float* __restrict__ contrib,
@@ -1112,11 +1120,11 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k
     // entry would be replayed whole, i.e. its records written twice with the same values
     const int tile = (int)(e & BQ_TILE);
     if (split) {
-        bwd_tile<2, true>(W, H, gx, tile, 2 * wid, (int)(2 * b + wid), ranges, point_list, slot_vals, rec, bg,
+        bwd_tile<2, true>(W, H, gx, tile, 2 * wid, (int)(2 * b + wid), ranges, point_list, goff, rec, bg,
                           alphas, n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written,
                           sh.srec[wid], &sh);
     } else {
-        bwd_tile<4, false>(W, H, gx, tile, 0, (int)(2 * b + wid), ranges, point_list, slot_vals, rec, bg, alphas,
+        bwd_tile<4, false>(W, H, gx, tile, 0, (int)(2 * b + wid), ranges, point_list, goff, rec, bg, alphas,
                            n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, sh.srec[wid],
                            nullptr, sh.stage[wid]);
     }
@@ -1132,7 +1140,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD1_WAVES))) k_render_bwd1(
     int W, int H, int gx, int T, uint32_t* __restrict__ sched,
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ slot_vals,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ goff,
     const float4* __restrict__ rec, const float* __restrict__ bg, const float* __restrict__ alphas,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ dL_dsegs,
     const float* __restrict__ dL_ddepths, const float* __restrict__ dL_dalphas, float* __restrict__ contrib,
@@ -1154,7 +1162,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD
     // a whole tile, or one of its list segments [0, ck) / [ck, depth) (publish_depth)
     const uint32_t kind = e & ~BQ_TILE;
     const int ck = (int)ts.sched[SCHED_CKPT];
-    bwd_tile<4, false>(W, H, gx, (int)(e & BQ_TILE), 0, (int)blockIdx.x, ranges, point_list, slot_vals, rec,
+    bwd_tile<4, false>(W, H, gx, (int)(e & BQ_TILE), 0, (int)blockIdx.x, ranges, point_list, goff, rec,
                        bg, alphas, n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, srec,
                        nullptr, stage, kind == BQ_BACK ? ck : 0, kind == BQ_FRONT ? ck : 0x7fffffff,
                        kind == BQ_FRONT ? ckpt : nullptr);
@@ -1184,7 +1192,7 @@ void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, 
 
 #if GSR_RENDER_PART != 1
 void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
-                            const uint2* ranges, const uint32_t* point_list, const uint32_t* slot_vals,
+                            const uint2* ranges, const uint32_t* point_list, const uint32_t* goff,
                             const float4* rec, const float* bg, const float* alpha, const uint32_t* n_contrib,
                             const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
                             const float* dL_dalpha, float* contrib, uint8_t* written, const float* ckpt,
@@ -1195,13 +1203,13 @@ void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order,
     if (split_bwd_depth() <= 0) {
         // up to two queue entries per tile (list segments); blocks past the queue return at once
         hipLaunchKernelGGL(k_render_bwd1, dim3(2 * T), dim3(64), 0, st, W, H, gx, T, sched, ranges, point_list,
-                           slot_vals, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha,
+                           goff, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha,
                            contrib, written, ckpt);
         return;
     }
     hipLaunchKernelGGL(k_render_bwd, dim3(T), dim3(128), 0, st, W, H, gx, T, split_bwd_depth(), sched, ranges,
                        point_list,
-                       slot_vals, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib,
+                       goff, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib,
                        written);
 }
 

@@ -291,7 +291,8 @@ def test_grid_wider_than_packed_rect(gpu_available, oracle_mod):
 def test_rows_binning_matches_radix_path(gpu_available, case):
     """binning_rows.hip (row-then-tile expansion, the default for grids <= 255 x 255
     tiles) and binning.hip's duplicate + radix tile sort build the same tile lists:
-    point_list, slot_vals, goff, ranges, n_contrib, images and gradients bit for bit."""
+    point_list, goff (every record slot is goff + the tile's place in the Gaussian's rectangle),
+    ranges, n_contrib, images and gradients bit for bit."""
     from diff_gaussian_rasterization import _C
     if case == "mt_small":
         scene, cam = synthetic_scene(60000, sh_degree=3, seed=41), orbit_camera(2, 640, 360, 400.0)
@@ -325,7 +326,7 @@ def test_rows_binning_matches_radix_path(gpu_available, case):
         rg = a["ranges"].reshape(gy, gx, 2)
         edge = rg[-1, :, :] if gy == 255 else rg[:, -1, :]
         assert int((edge[..., 1] > edge[..., 0]).sum()) > 0, "no Gaussian reaches the 255th tile row / column"
-    for k in ("point_list", "slot_vals", "ranges", "n_contrib", "color", "depth", "alpha", "segment", "radii"):
+    for k in ("point_list", "ranges", "n_contrib", "color", "depth", "alpha", "segment", "radii"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
     vis = a["radii"] > 0  # the row path writes goff for visible Gaussians only
     np.testing.assert_array_equal(a["goff"][vis], b["goff"][vis], err_msg="goff")
