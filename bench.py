@@ -51,7 +51,8 @@ SIMD_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 # newest committed counter summary (tools/pmc.sh + tools/pmc_summary.py); its counter-derived
 # fields are reported only when it was collected on the sources being benchmarked
 PMC_SUMMARY = next((os.path.join(ROOT, "profiles", f) for f in
-                    ("round4_pmc_summary.json", "round3_pmc_summary.json", "round2_pmc_summary.json", "round1_pmc_summary.json")
+                    ("round5_pmc_summary.json", "round4_pmc_summary.json", "round3_pmc_summary.json",
+                     "round2_pmc_summary.json", "round1_pmc_summary.json")
                     if os.path.exists(os.path.join(ROOT, "profiles", f))), "")
 
 

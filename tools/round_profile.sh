@@ -11,10 +11,16 @@ O=gpurun_out/$TAG
 rm -rf $O; mkdir -p $O
 timeout -k 10 900 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -30 $O/pytest_gpu.log; exit 1; }
 tail -2 $O/pytest_gpu.log
-timeout -k 10 400 python bench.py --stages > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
+# the driver's bench command, then the same command under the profiler (its kernel statistics are
+# the ones the line's roofline avg_launch_ms must agree with)
+timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 --stages > $O/bench.json 2> $O/bench.err || { tail -30 $O/bench.err; exit 1; }
 cat $O/bench.json; grep -v amdgpu.ids $O/bench.err
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof -o kt --output-format csv -- python3 bench.py --steps 30 --warmup 5 --no-cpu-baseline --no-train --batched-views 1 > $O/prof_bench.log 2>&1 || { tail -20 $O/prof_bench.log; exit 1; }
+timeout -k 10 400 python bench.py --stages > $O/bench_200.json 2> $O/bench_200.err || { tail -30 $O/bench_200.err; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o kt --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/prof_bench.json 2> $O/prof_bench.log || { tail -20 $O/prof_bench.log; exit 1; }
 cp $(find $O/prof -name "*kernel_stats.csv" | head -1) $O/kernel_stats.csv
 python tools/kstats.py $O/kernel_stats.csv
 bash tools/pmc.sh > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
-python tools/pmc_summary.py $O/pmc_summary.json | grep -E "^render|^gaussian|^preprocess"
+python tools/pmc_summary.py $O/pmc_summary.json | grep -E "^render|^gaussian|^preprocess|^k_tiles|^k_rows"
+GSR_DIST_BACKEND=gloo timeout -k 10 400 python3 bench.py --gpus 2 --steps 20 --warmup 5 --no-train > $O/gloo2.json 2> $O/gloo2.err || { tail -20 $O/gloo2.err; exit 1; }
+bash tools/configs_bench.sh > $O/configs.txt 2>&1 || { tail -20 $O/configs.txt; exit 1; }
+cat $O/configs.txt
