@@ -19,6 +19,7 @@ timeout -k 10 400 python bench.py --stages > $O/bench_200.json 2> $O/bench_200.e
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $O/prof -o kt --output-format csv -- python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/prof_bench.json 2> $O/prof_bench.log || { tail -20 $O/prof_bench.log; exit 1; }
 cp $(find $O/prof -name "*kernel_stats.csv" | head -1) $O/kernel_stats.csv
 python tools/kstats.py $O/kernel_stats.csv
+for k in k_render_bwd1 k_render_fwd; do python tools/ktrace_phases.py $(find $O/prof -name "*kernel_trace.csv" | head -1) $k; done | tee $O/kernel_phases.txt
 bash tools/pmc.sh > $O/pmc.log 2>&1 || { tail -20 $O/pmc.log; exit 1; }
 python tools/pmc_summary.py $O/pmc_summary.json | grep -E "^render|^gaussian|^preprocess|^k_tiles|^k_rows"
 GSR_DIST_BACKEND=gloo timeout -k 10 400 python3 bench.py --gpus 2 --steps 20 --warmup 5 --no-train > $O/gloo2.json 2> $O/gloo2.err || { tail -20 $O/gloo2.err; exit 1; }
