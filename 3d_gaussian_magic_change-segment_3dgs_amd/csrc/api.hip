@@ -371,7 +371,7 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
         launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
                           at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect),
                           packed ? at<uint32_t>(g, L.rect32) : nullptr, at<float>(g, L.shjac), at<float>(g, L.opac),
-                          g + L.ws, lb ? sort_zero_bytes(P, depth_sort_passes()) : 0,
+                          at<uint32_t>(g, L.goff), at<uint32_t>(g, L.btot), g + L.ws, lb ? sort_zero_bytes(P, depth_sort_passes()) : 0,
                           g + L.ws_scan, scan_ws_bytes(P), st);
     }
     GSR_STAGE("preprocess");
@@ -385,7 +385,8 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
         // k_radix_hist 2 us: 10.5 -> 12.6 us)
         const bool tally = P <= TALLY_MAX_P;
         const SortFinal nokeys{nullptr, nullptr, 0, true, tally ? at<uint32_t>(g, L.tiles_touched) : nullptr,
-                               tally ? hs.dev : nullptr, &tallied};
+                               tally ? hs.dev : nullptr, &tallied, at<uint32_t>(g, L.btot),
+                               at<uint32_t>(g, L.bbase), (uint32_t)cdiv((size_t)P, (size_t)SLOT_BLOCK)};
         launch_radix_sort(at<uint32_t>(g, L.depth_keys), nullptr, at<uint32_t>(g, L.dkeys_alt),
                           at<uint32_t>(g, L.order_alt), at<uint32_t>(g, L.depth_keys), at<uint32_t>(g, L.order), P,
                           32, g + L.ws, /*ws_zeroed=*/true, st, packed ? at<uint32_t>(g, L.rect32) : nullptr,
@@ -465,7 +466,7 @@ int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* b
             const uint32_t* n_total = at<uint32_t>(g, GL.offsets) + (P - 1);
             auto rb = [&](int stage) {
                 launch_rows_binning(P, IL.gx, IL.gy, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets),
-                                    at<uint32_t>(g, GL.rect32_sorted), at<uint32_t>(g, GL.goff), g + GL.ws, b + BL.ws,
+                                    at<uint32_t>(g, GL.rect32_sorted), g + GL.ws, b + BL.ws,
                                     at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.vals_alt),
                                     at<uint32_t>(b, BL.point_list), ranges, order, at<uint4>(b, BL.written),
                                     cdiv(cap, 16), cap, n_total, st, stage, /*fused=*/true,
@@ -492,8 +493,8 @@ int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* b
                 launch_duplicate(P, at<uint32_t>(g, GL.order), at<uint32_t>(g, GL.offsets),
                                  at<uint32_t>(g, GL.tiles_touched), at<ushort4>(g, GL.rect),
                                  rect_packable(IL.gx, IL.gy) ? at<uint32_t>(g, GL.rect32_sorted) : nullptr, IL.gx,
-                                 at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid), at<uint32_t>(g, GL.goff),
-                                 ranges, T, (uint32_t)cap, st);
+                                 at<uint32_t>(b, BL.tkeys), at<uint32_t>(b, BL.slot_gid), ranges, T, (uint32_t)cap,
+                                 st);
             }
             GSR_STAGE("duplicate");
             const int bits = (int)higher_msb((uint32_t)T);
@@ -623,7 +624,7 @@ int backward_impl(const gsr_settings* s, const gsr_inputs* in, const int* radii,
             StageScope sc(GSR_STAGE_RENDER_BWD, st);
             launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order),
                                    at<uint32_t>(im, IL.order) + IL.gx * IL.gy, at<uint2>(im, IL.ranges),
-                                   at<uint32_t>(b, BL.point_list), at<uint32_t>(g, GL.goff),
+                                   at<uint32_t>(b, BL.point_list), at<uint32_t>(g, GL.bbase),
                                    at<float4>(g, GL.rec), s->bg, alpha, at<uint32_t>(im, IL.n_contrib), dL_dcolor,
                                    dL_dsegment, dL_ddepth, dL_dalpha, contrib, written, at<float>(im, IL.ckpt), st);
         }
@@ -634,6 +635,7 @@ int backward_impl(const gsr_settings* s, const gsr_inputs* in, const int* radii,
         gsr_grads gr = *grads;
         if (sh_rows) gr.dsh = nullptr;  // deferred: the exchange writes dsh from the rows
         launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
+                                 at<uint32_t>(g, GL.bbase),
                                  at<uint8_t>(g, GL.clamped), contrib, written, at<float>(g, GL.opac),
                                  at<float>(g, GL.shjac), gr, sh_rows, st);
     }
@@ -754,7 +756,7 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
                 launch_render_backward(s->W, s->H, IL.gx, IL.gy, at<uint32_t>(im, IL.order),
                                        at<uint32_t>(im, IL.order) + IL.gx * IL.gy, at<uint2>(im, IL.ranges),
                                        at<uint32_t>(b, BL.point_list),
-                                       at<uint32_t>(g, GL.goff), at<float4>(g, GL.rec), s->bg, V.alpha,
+                                       at<uint32_t>(g, GL.bbase), at<float4>(g, GL.rec), s->bg, V.alpha,
                                        at<uint32_t>(im, IL.n_contrib), V.dL_dcolor, V.dL_dsegment, V.dL_ddepth,
                                        V.dL_dalpha, contrib, written, at<float>(im, IL.ckpt), sv);
             }
@@ -770,6 +772,7 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
         w.radii = V.radii;
         w.tiles_touched = at<uint32_t>(g, GL.tiles_touched);
         w.goff = at<uint32_t>(g, GL.goff);
+        w.bbase = at<uint32_t>(g, GL.bbase);
         w.clamped = at<uint8_t>(g, GL.clamped);
         w.contrib = contrib;
         w.written = written;
@@ -881,6 +884,7 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
     else if (n == "clamped") G(GL.clamped, Pz);
     else if (n == "order") G(GL.order, Pz * 4);
     else if (n == "goff") G(GL.goff, Pz * 4);
+    else if (n == "bbase") G(GL.bbase, cdiv(Pz, (size_t)SLOT_BLOCK) * 4);
     else if (n == "point_list") B(BL.point_list, I * 4);
     else if (n == "slot_vals") B(BL.slot_vals, I * 4);
     else if (n == "written") B(BL.written, I);  // the backward's written-record flags (1 byte per slot)

@@ -287,13 +287,62 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
 __device__ __forceinline__ bool identity_pass(const uint32_t* span, int shift, int bits) {
     return (((span[0] & span[1]) >> shift) & ((1u << bits) - 1u)) == 0u;
 }
+// Record-slot block bases (gsr_internal.h SLOT_BLOCK): bbase[b] = sum of btot[0, b), b < nb, by one
+// block of HIST_THREADS threads: thread t scans a run of up to BB_RUN consecutive totals, all loaded
+// up front (one load latency per round of HIST_THREADS x BB_RUN totals, i.e. one round up to 2.1M
+// Gaussians), the runs' sums are scanned across the block.
+constexpr int BB_RUN = 8;
+__device__ void block_bases(const uint32_t* __restrict__ btot, uint32_t nb, uint32_t* __restrict__ bbase) {
+    __shared__ uint32_t s_w[HIST_THREADS / 64];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    uint32_t carry = 0;
+    for (uint32_t r0 = 0; r0 < nb; r0 += BB_RUN * HIST_THREADS) {
+        const uint32_t per = min((uint32_t)BB_RUN, (nb - r0 + HIST_THREADS - 1) / HIST_THREADS);  // uniform
+        const uint32_t i0 = r0 + per * threadIdx.x;
+        uint32_t v[BB_RUN], s = 0;
+#pragma unroll
+        for (int k = 0; k < BB_RUN; ++k) {
+            v[k] = (uint32_t)k < per && i0 + k < nb ? btot[i0 + k] : 0u;
+            s += v[k];
+        }
+        uint32_t x = s;
+#pragma unroll
+        for (int o = 1; o < 64; o <<= 1) {
+            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+            if (lane >= o) x += y;
+        }
+        if (lane == 63) s_w[wid] = x;
+        __syncthreads();
+        uint32_t pre = carry, tot = 0;
+#pragma unroll
+        for (int w = 0; w < HIST_THREADS / 64; ++w) {
+            pre += w < wid ? s_w[w] : 0u;
+            tot += s_w[w];
+        }
+        __syncthreads();  // s_w is reused by the next round
+        pre += x - s;
+#pragma unroll
+        for (int k = 0; k < BB_RUN; ++k) {
+            if ((uint32_t)k < per && i0 + k < nb) bbase[i0 + k] = pre;
+            pre += v[k];
+        }
+        carry += tot;
+    }
+}
+__global__ void __launch_bounds__(HIST_THREADS) k_block_bases(const uint32_t* __restrict__ btot, uint32_t nb,
+                                                              uint32_t* __restrict__ bbase) {
+    block_bases(btot, nb, bbase);
+}
+
 template <int HIST_ITEMS>
 __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __restrict__ keys, size_t n,
                                                              int passes, int per_pass, int key_bits,
                                                              uint32_t* __restrict__ hist, uint32_t* span,
                                                              int skip_sentinel, const uint32_t* n_dev,
                                                              const uint32_t* __restrict__ tally,
-                                                             unsigned long long* tally_word, uint32_t* tally_host) {
+                                                             unsigned long long* tally_word, uint32_t* tally_host,
+                                                             const uint32_t* __restrict__ bb_tot, uint32_t bb_n,
+                                                             uint32_t* __restrict__ bb_base) {
     ST_T(st0)
     if (n_dev) n = min(n, (size_t)*n_dev);
     __shared__ uint32_t cnt[4][RADIX];
@@ -378,6 +427,7 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
         for (int p = 0; p < passes; ++p)
             if (cnt[p][threadIdx.x]) atomicAdd(&hist[p * RADIX + threadIdx.x], cnt[p][threadIdx.x]);
     if (threadIdx.x < 2 && s_span[threadIdx.x]) atomicOr(&span[threadIdx.x], s_span[threadIdx.x]);
+    if (bb_base && blockIdx.x == 0) block_bases(bb_tot, bb_n, bb_base);  // block-uniform
 #ifdef GSR_SORT_TRACE
     __syncthreads();
     if (threadIdx.x == 0 && blockIdx.x < 1024) {
@@ -813,7 +863,7 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
                                                    const ushort4* __restrict__ rect,
                                                    const uint32_t* __restrict__ rect_sorted, int gx,
                                                    uint32_t* __restrict__ tkeys, uint32_t* __restrict__ slot_gid,
-                                                   uint32_t* __restrict__ goff, uint2* __restrict__ ranges, int T,
+                                                   uint2* __restrict__ ranges, int T,
                                                    uint32_t cap) {
     __shared__ uint32_t s_key[DUP_CAP], s_gid[DUP_CAP];
     // ranges start at {~0u, 0} for the tile sort's atomicMin / atomicMax; empty tiles end
@@ -844,7 +894,6 @@ __global__ void __launch_bounds__(256) k_duplicate(int P, const uint32_t* __rest
         }
         if (cnt != 0) {
             uint32_t off = r == 0 ? 0u : offsets[r - 1];
-            goff[g] = off;
             if (staged) {
                 uint32_t lo = off - bbase;
                 for (int y = rc.y; y < rc.w; ++y)
@@ -1121,7 +1170,11 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
                            n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel, n_dev,
                            tally ? final_out->tally : nullptr,
                            reinterpret_cast<unsigned long long*>(W.counter + TALLY_WORD),
-                           final_out ? final_out->tally_host : nullptr);
+                           final_out ? final_out->tally_host : nullptr, final_out ? final_out->bb_tot : nullptr,
+                           final_out ? final_out->bb_n : 0u, final_out ? final_out->bb_base : nullptr);
+    } else if (final_out && final_out->bb_base && final_out->bb_n) {
+        hipLaunchKernelGGL(k_block_bases, dim3(1), dim3(HIST_THREADS), 0, st, final_out->bb_tot, final_out->bb_n,
+                           final_out->bb_base);
     }
     if (grp) {
         // grouped look-back passes with the pass plan on the device (k_radix_scatter_grp)
@@ -1223,10 +1276,10 @@ void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st) {
 
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, const uint32_t* rect_sorted, int gx, uint32_t* tkeys,
-                      uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, uint32_t cap, hipStream_t st) {
+                      uint32_t* slot_gid, uint2* ranges, int T, uint32_t cap, hipStream_t st) {
     if (P == 0) return;
     hipLaunchKernelGGL(k_duplicate, dim3(cdiv(P, 256)), dim3(256), 0, st, P, order, offsets, tiles_touched, rect,
-                       rect_sorted, gx, tkeys, slot_gid, goff, ranges, T, cap);
+                       rect_sorted, gx, tkeys, slot_gid, ranges, T, cap);
 }
 
 

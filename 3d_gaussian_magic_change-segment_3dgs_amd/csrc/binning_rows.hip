@@ -9,9 +9,9 @@
 // order[r], the packed tile rectangle rect[r] = x0 | y0 << 8 | x1 << 16 | y1 << 24 and
 // the inclusive scan offsets[r] of the tile counts (the instance slots of r start at
 // offsets[r - 1]).  Output: point_list (Gaussian ids grouped by tile, by depth inside a
-// tile: the reference's sorted (tile << 32 | depth) order, bit for bit), slot_vals (each
-// entry's instance slot u = goff + (y - y0) w + (x - x0), the slot the backward's record
-// goes to), goff, ranges and the heavy-first tile order.
+// tile: the reference's sorted (tile << 32 | depth) order, bit for bit), ranges and the
+// heavy-first tile order.  (An instance's record slot is not written here: the render backward
+// forms it from the Gaussian's first slot and its rectangle, gsr_internal.h SLOT_BLOCK.)
 //
 //   level 1 (rows):  Gaussian r -> one entry per tile row y0..y1-1 of its rectangle,
 //                    grouped by row, in depth order inside a row;
@@ -27,8 +27,8 @@
 //            bits below its own (stable and deterministic, no ordered atomics); the
 //            chunk's output is assembled in LDS in bucket order and written as runs.
 // Level-2 chunks never straddle rows (row y's entries form ceil(R_y / RB_CH) chunks), so
-// a chunk's buckets are the gx columns of one row.  Bytes per instance: 8 written
-// (point_list, slot_vals) plus ~12 written and read per row entry (~2.9 instances each at
+// a chunk's buckets are the gx columns of one row.  Bytes per instance: 4 written
+// (point_list) plus ~12 written and read per row entry (~2.9 instances each at
 // the metric scene), against ~52 for duplicate + two radix passes over (key, slot, id).
 #include "gsr_internal.h"
 
@@ -195,9 +195,7 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_count(int P, int gy, int nch1, 
     zero16(zero, nzero16, (size_t)blockIdx.x * RB_CH1 + threadIdx.x, (size_t)gridDim.x * RB_CH1);
 }
 
-// Level-1 entries (E1, grouped by row): e_gid = Gaussian id, e_x = x0 | x1 << 8.  Also goff[gid],
-// the Gaussian's first record slot (its instance (x, y) has slot goff + (y - y0) w + (x - x0): the
-// render backward forms it from goff and the rectangle in the Gaussian's record).
+// Level-1 entries (E1, grouped by row): e_gid = Gaussian id, e_x = x0 | x1 << 8.
 // Dynamic LDS: bits + pre, 2 x gy x RB_S1 words, sized by the grid rather than the 255
 // bound (gy = 68 at 1080p: 18 KB; 67 KB at gy = 255, covered by the 4080-px-tall case of
 // tests/test_gpu_parity.py::test_rows_binning_matches_radix_path).  Every global load is
@@ -210,7 +208,7 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_count(int P, int gy, int nch1, 
 __global__ void __launch_bounds__(RB_CH1) k_rows_scatter(int P, int gy, int nch1, const uint32_t* __restrict__ order,
                                                         uint32_t* __restrict__ offsets,
                                                         const uint32_t* __restrict__ rect,
-                                                        const uint32_t* __restrict__ base1, uint32_t* __restrict__ goff,
+                                                        const uint32_t* __restrict__ base1,
                                                         uint32_t* __restrict__ e_gid,
                                                         uint32_t* __restrict__ e_x, uint32_t cap, int fused,
                                                         uint32_t* host_total) {
@@ -260,7 +258,6 @@ __global__ void __launch_bounds__(RB_CH1) k_rows_scatter(int P, int gy, int nch1
     lds_scan256(cnt, gy, lst, &tot);
     const bool staged = tot <= (uint32_t)RB_STAGE1;  // uniform
     if (vis) {
-        goff[g] = off;
         const uint32_t below = bit - 1u;
         for (int y = y0; y < y1; ++y) {
             const uint32_t rank = pre[y * RB_S1 + wd] + (uint32_t)__popc(bits[y * RB_S1 + wd] & below);
@@ -536,7 +533,7 @@ size_t rows_bin_ws_bytes(size_t cap) {
 }
 
 void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, uint32_t* offsets, const uint32_t* rect,
-                         uint32_t* goff, void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_x,
+                         void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_x,
                          uint32_t* point_list, uint2* ranges, uint32_t* tile_order,
                          uint4* written, size_t written16, size_t cap, const uint32_t* n_total, hipStream_t st,
                          int stage, bool fused, uint32_t* host_total) {
@@ -563,7 +560,7 @@ void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, uint32_t*
                            cdiv(S1.bytes, 16), (int)fused);
         launch_scan_exclusive(table1, base1, n1, nullptr, S1, st);
         hipLaunchKernelGGL(k_rows_scatter, dim3(nch1), dim3(RB_CH1), 2 * gy * RB_S1 * 4, st, P, gy, nch1, order,
-                           offsets, rect, base1, goff, e_gid, e_x, cap32, (int)fused, host_total);
+                           offsets, rect, base1, e_gid, e_x, cap32, (int)fused, host_total);
     } else if (stage == 1) {  // level 2: tiles (+ ranges)
         const int grid2 = (int)std::min<size_t>(RB_GRID2, gy + cdiv(cap, RB_CH));
         hipLaunchKernelGGL(k_tiles_count, dim3(grid2), dim3(RB_CH), 0, st, gx, gy, nch1, table1, base1, e_x, table2,

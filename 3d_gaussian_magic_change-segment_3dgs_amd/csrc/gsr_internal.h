@@ -132,8 +132,13 @@ size_t rows_bin_ws_bytes(size_t cap);
 // ---- geometry buffer (reference GeometryState, rasterizer_impl.cu:155-171) ----
 struct GeomLayout {
     size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, goff, ws,
-        ws_scan, rect32, rect32_alt, rect32_sorted, shjac, opac, bytes;
+        ws_scan, rect32, rect32_alt, rect32_sorted, shjac, opac, btot, bbase, bytes;
 };
+// Record slots are numbered in Gaussian-index order, per block of SLOT_BLOCK Gaussians (the
+// preprocess's blocks): Gaussian g's instance slots start at goff[g] + bbase[g / SLOT_BLOCK], where
+// goff is the exclusive scan of the tile counts inside g's block and bbase[b] the slots of the
+// blocks before b (block_bases, binning.hip, from the blocks' totals btot).
+constexpr int SLOT_BLOCK = 256;
 inline GeomLayout geom_layout(size_t P) {
     GeomLayout L{};
     size_t o = 0;
@@ -163,6 +168,8 @@ inline GeomLayout geom_layout(size_t P) {
     // opacity of each visible Gaussian, for the per-Gaussian backward (which recomputes the
     // conic and so reads no 64-B record: the record's 32-B half cost a scattered sector read)
     L.opac = take(P * 4);
+    L.btot = take(cdiv(P, (size_t)SLOT_BLOCK) * 4);
+    L.bbase = take(cdiv(P, (size_t)SLOT_BLOCK) * 4);
     L.bytes = o + ALIGN;
     return L;
 }
@@ -258,8 +265,8 @@ inline char* aligned_base(void* p) {
 // preprocess.hip
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec,
                        int* radii, uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped,
-                       ushort4* rect, uint32_t* rect32, float* shjac, float* opac, void* zero_a, size_t zero_a_bytes,
-                       void* zero_b, size_t zero_b_bytes, hipStream_t st);
+                       ushort4* rect, uint32_t* rect32, float* shjac, float* opac, uint32_t* goff, uint32_t* btot,
+                       void* zero_a, size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes, hipStream_t st);
 // the packed rect (GeomLayout::rect32) fits grids of up to 255 x 255 tiles (4080 px)
 inline bool rect_packable(int gx, int gy) { return gx <= 255 && gy <= 255; }
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st);
@@ -268,6 +275,7 @@ struct MvView {
     const int* radii;
     const uint32_t* tiles_touched;
     const uint32_t* goff;
+    const uint32_t* bbase;
     const uint8_t* clamped;
     const float* contrib;
     const uint8_t* written;
@@ -295,8 +303,8 @@ void launch_gaussian_backward_multiview(int P, int D, int M, float scale_modifie
 void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const float* shx, float* dsh,
                         hipStream_t st);
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
-                              const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const uint8_t* written, const float* opac,
+                              const uint32_t* tiles_touched, const uint32_t* goff, const uint32_t* bbase,
+                              const uint8_t* clamped, const float* contrib, const uint8_t* written, const float* opac,
                               const float* shjac, const gsr_grads& g, float* shx, hipStream_t st);
 // binning.hip
 // Optional last-pass outputs of a sort: ranges[key] = [first, last + 1) of each key's run in
@@ -317,6 +325,12 @@ struct SortFinal {
     const uint32_t* tally = nullptr;
     uint32_t* tally_host = nullptr;
     bool* tally_used = nullptr;
+    // optional: the record slots' block bases (SLOT_BLOCK): bb_base[b] = sum of bb_tot[0, b) for
+    // b < bb_n, computed by the histogram kernel's block 0 (or a one-block kernel when the sort
+    // runs without it)
+    const uint32_t* bb_tot = nullptr;
+    uint32_t* bb_base = nullptr;
+    uint32_t bb_n = 0;
 };
 void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in /*NULL = identity*/, uint32_t* keys_tmp,
                        uint32_t* vals_tmp, uint32_t* keys_out, uint32_t* vals_out, size_t n, int key_bits,
@@ -354,20 +368,20 @@ void launch_scan_inclusive_gather(const uint32_t* src, const uint32_t* gather_id
 void launch_scan_exclusive(const uint32_t* src, uint32_t* out, size_t n, const uint32_t* n_dev, const ScanWs& W,
                            hipStream_t st);
 // binning_rows.hip: tile lists by row-then-tile expansion (grids up to 255 x 255 tiles).
-// stage 0: level 1 (rows, goff); 1: level 2 (point_list, written flags
+// stage 0: level 1 (rows); 1: level 2 (point_list, written flags
 // cleared); 2: ranges + heavy-first tile order.  geom_ws: rows_bin_geom_ws_bytes(P, gy)
 // bytes (the depth sort's workspace, free by then); bin_ws: rows_bin_ws_bytes(cap).
 // fused: level 1 also computes the depth-ordered instance offsets (written to offsets, as the
 // depth-order scan writes them; num_rendered also to host_total when non-NULL), so the scan need
 // not run first.
 void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, uint32_t* offsets, const uint32_t* rect,
-                         uint32_t* goff, void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_x,
+                         void* geom_ws, void* bin_ws, uint32_t* e_gid, uint32_t* e_x,
                          uint32_t* point_list, uint2* ranges, uint32_t* tile_order,
                          uint4* written, size_t written16, size_t cap, const uint32_t* n_total, hipStream_t st,
                          int stage, bool fused, uint32_t* host_total);
 void launch_duplicate(int P, const uint32_t* order, const uint32_t* offsets, const uint32_t* tiles_touched,
                       const ushort4* rect, const uint32_t* rect_sorted, int gx, uint32_t* tkeys,
-                      uint32_t* slot_gid, uint32_t* goff, uint2* ranges, int T, uint32_t cap, hipStream_t st);
+                      uint32_t* slot_gid, uint2* ranges, int T, uint32_t cap, hipStream_t st);
 // render.hip
 // sched = order + T (TileSched).  Forward grid 2T single-wave blocks in the heavy-first
 // order (split tiles first); backward grid T two-wave blocks over the forward's depth
@@ -377,7 +391,7 @@ void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, 
                            float* out_color, float* out_depth, float* out_alpha, float* out_segment,
                            uint32_t* n_contrib, float* ckpt, hipStream_t st);
 void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
-                            const uint2* ranges, const uint32_t* point_list, const uint32_t* goff,
+                            const uint2* ranges, const uint32_t* point_list, const uint32_t* bbase,
                             const float4* rec, const float* bg, const float* alpha, const uint32_t* n_contrib,
                             const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
                             const float* dL_dalpha, float* contrib, uint8_t* written, const float* ckpt,

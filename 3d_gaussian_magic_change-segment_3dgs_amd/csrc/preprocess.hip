@@ -158,6 +158,16 @@ typedef float sh_v4 __attribute__((ext_vector_type(4)));
 // pass's writes.  Without block barriers the four waves of a block no longer wait for each other
 // at every pass, so their loads overlap more.
 __device__ __forceinline__ void wave_lds_fence() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+// Inclusive scan over the wave with DPP (row_shr inside 16-lane rows, then row_bcast 15 / 31).
+__device__ __forceinline__ uint32_t wave_scan_incl(uint32_t x) {
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x118, 0xF, 0xF, true);  // row_shr:8
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false); // row_bcast:15
+    x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x143, 0xC, 0xF, false); // row_bcast:31
+    return x;
+}
 
 #ifdef GSR_BLOCK_SYNC  // (A/B: the block barriers the fence replaced)
 #define GSR_WAVE_SYNC() __syncthreads()
@@ -339,7 +349,8 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
                                                     uint32_t* __restrict__ depth_keys,
                                                     uint8_t* __restrict__ clamped, ushort4* __restrict__ rect,
                                                     uint32_t* __restrict__ rect32, float* __restrict__ shjac,
-                                                    float* __restrict__ opac,
+                                                    float* __restrict__ opac, uint32_t* __restrict__ goff,
+                                                    uint32_t* __restrict__ btot,
                                                     void* zero_a, size_t zero_a16, void* zero_b, size_t zero_b16) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
     // clear the depth sort's and the scan's look-back counters (saves two memset launches)
@@ -404,6 +415,28 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     if (ok) get_rect(px, py, (int)my_radius, gx, gy, x0, y0, x1, y1);
     const uint32_t ntiles = (uint32_t)((x1 - x0) * (y1 - y0));
     ok = ok && ntiles != 0;
+    // Record slots in Gaussian-index order: the block's exclusive scan of the tile counts here,
+    // the blocks' bases from their totals btot in the depth sort's histogram kernel (bbase, see
+    // block_bases): Gaussian idx's first slot is goff[idx] + bbase[idx / 256].  Neighbouring
+    // Gaussians then own neighbouring slot ranges, which the per-Gaussian backward reads.  The wave
+    // scan (DPP) runs here, the block combine after the SH work (slot_scan_finish), behind a bare
+    // s_barrier: __syncthreads' fence would also wait for the SH loads in flight.
+    __shared__ uint32_t s_wtot[4];
+    const uint32_t t_ok = ok ? ntiles : 0u;
+    const uint32_t t_incl = wave_scan_incl(t_ok);
+    if (lane == 63) s_wtot[wave] = t_incl;
+    auto slot_scan_finish = [&]() {
+        wave_lds_fence();
+        __builtin_amdgcn_s_barrier();
+        wave_lds_fence();
+        uint32_t pre = 0;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) pre += w < wave ? s_wtot[w] : 0u;
+        const uint32_t slot = pre + t_incl - t_ok;
+        if (threadIdx.x == 0) btot[blockIdx.x] = s_wtot[0] + s_wtot[1] + s_wtot[2] + s_wtot[3];
+        if (live) goff[idx] = slot;
+        return slot;
+    };
 
     f3 rgb = {0.f, 0.f, 0.f};
     uint8_t cbits = 0;
@@ -470,6 +503,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     } else if (ok) {
         rgb = ld3(in.colors_precomp + 3 * (size_t)idx);
     }
+    const uint32_t slot0 = slot_scan_finish();
     if (!ok) {  // culled (the reference's early returns): no tiles, sorted last
         if (live) {
             radii[idx] = 0;
@@ -497,7 +531,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     // record's second 32-B sector was a partial write (read-modify-write in memory; rocprof, round
     // 5: C5 preprocess 540 -> 447 us, the metric scene 69.1 -> 68.1 us).
     R[3] = make_float4(__uint_as_float((uint32_t)x0 | ((uint32_t)y0 << 16)),
-                       __uint_as_float((uint32_t)x1 | ((uint32_t)y1 << 16)), 0.f, 0.f);
+                       __uint_as_float((uint32_t)x1 | ((uint32_t)y1 << 16)), __uint_as_float(slot0), 0.f);
     radii[idx] = (int)my_radius;
     opac[idx] = opacity;
     tiles_touched[idx] = ntiles;
@@ -588,6 +622,84 @@ __device__ __forceinline__ void sum_records(const float* __restrict__ contrib, c
     for (int j = 0; j < 12; ++j) q[j] = (float)d[j];
 }
 
+// Wave-cooperative form of sum_records for slots in Gaussian-index order (gsr_internal.h
+// SLOT_BLOCK): the 64 lanes' ranges [lo, lo + n) tile one contiguous slot range, so the wave reads
+// its written flags as one run (lane l: granule l of 16 slots, 1024 slots per round), lists the
+// written slots in LDS by a wave scan, loads their records with one lane per record, and every lane
+// then sums its own from LDS -- in slot order, in fp64, as sum_records: the same bits.  Every lane
+// of the wave must call it (n = 0 for a lane without records).  W: the wave's LDS.
+struct GatherLds {
+    uint32_t gran[64];    // per granule: (written slots of the round before it) << 16 | its 16-bit mask
+    uint16_t list[1024];  // the round's written slots, as offsets from the round's first slot
+    float4 recs[64][3];   // one batch of their records
+};
+__device__ __forceinline__ void wave_gather(const float* __restrict__ contrib, const uint8_t* __restrict__ written,
+                                            uint32_t lo, uint32_t n, float q[12], GatherLds& W) {
+    const int lane = threadIdx.x & 63;
+    double d[12];
+#pragma unroll
+    for (int j = 0; j < 12; ++j) d[j] = 0.0;
+    const uint32_t hi = lo + n;
+    // the wave's range [L, H): the ranges of lanes with records are ordered and adjacent
+    uint32_t L = n ? lo : 0xFFFFFFFFu, H = n ? hi : 0u;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        L = min(L, (uint32_t)__shfl_xor((int)L, o, 64));
+        H = max(H, (uint32_t)__shfl_xor((int)H, o, 64));
+    }
+    L = __builtin_amdgcn_readfirstlane(L);
+    H = __builtin_amdgcn_readfirstlane(H);
+    const uint4* w16 = reinterpret_cast<const uint4*>(written);
+    auto fold8 = [](uint64_t f) { return (uint32_t)(((f & 0x0101010101010101ull) * 0x0102040810204080ull) >> 56); };
+    for (uint32_t base = L & ~15u; base < H; base += 1024) {  // wave-uniform (L = ~0 when no lane has records)
+        const uint32_t s0 = base + 16u * (uint32_t)lane;
+        uint32_t m = 0;
+        if (s0 < H) {
+            const uint4 f = w16[s0 >> 4];
+            m = fold8((uint64_t)f.x | ((uint64_t)f.y << 32)) | fold8((uint64_t)f.z | ((uint64_t)f.w << 32)) << 8;
+            if (L > s0) m &= 0xFFFFu << min(L - s0, 16u);
+            if (H - s0 < 16u) m &= (1u << (H - s0)) - 1u;
+        }
+        const uint32_t c = (uint32_t)__popc(m);
+        const uint32_t incl = wave_scan_incl(c), excl = incl - c;
+        const uint32_t total = (uint32_t)__builtin_amdgcn_readlane((int)incl, 63);
+        W.gran[lane] = (excl << 16) | m;
+        for (uint32_t mm = m, k = excl; mm; mm &= mm - 1, ++k)
+            W.list[k] = (uint16_t)(16u * (uint32_t)lane + (uint32_t)__builtin_ctz(mm));
+        wave_lds_fence();
+        // this lane's list positions [a, b) in the round
+        auto pos = [&](uint32_t sl) -> uint32_t {
+            if (sl <= base) return 0u;
+            const uint32_t off = sl - base;
+            if (off >= 1024u) return total;
+            const uint32_t g = W.gran[off >> 4];
+            return (g >> 16) + (uint32_t)__popc((g & 0xFFFFu) & ((1u << (off & 15u)) - 1u));
+        };
+        const uint32_t a = n ? pos(lo) : 0u, b = n ? pos(hi) : 0u;
+        for (uint32_t r0 = 0; r0 < total; r0 += 64) {  // wave-uniform
+            if (r0 + (uint32_t)lane < total) {
+                const float4* src = reinterpret_cast<const float4*>(
+                    contrib + (size_t)(base + W.list[r0 + lane]) * CONTRIB_STRIDE);
+                const float4 x0 = src[0], x1 = src[1], x2 = src[2];
+                W.recs[lane][0] = x0;
+                W.recs[lane][1] = x1;
+                W.recs[lane][2] = x2;
+            }
+            wave_lds_fence();
+            const uint32_t j0 = max(a, r0), j1 = min(b, r0 + 64u);
+            for (uint32_t j = j0; j < j1; ++j) {
+                const float4 x0 = W.recs[j - r0][0], x1 = W.recs[j - r0][1], x2 = W.recs[j - r0][2];
+                d[0] += x0.x; d[1] += x0.y; d[2] += x0.z; d[3] += x0.w;
+                d[4] += x1.x; d[5] += x1.y; d[6] += x1.z; d[7] += x1.w;
+                d[8] += x2.x; d[9] += x2.y; d[10] += x2.z; d[11] += x2.w;
+            }
+            wave_lds_fence();  // the batch is read before the next one overwrites it
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 12; ++j) q[j] = (float)d[j];
+}
+
 #if GSR_PRE_PART == 2
 // ----------------------------------------------------------------- backward --
 // One thread per Gaussian.  Sums the per-(tile, Gaussian) gradient records that
@@ -602,10 +714,16 @@ __device__ __forceinline__ void sum_records(const float* __restrict__ contrib, c
 //   dopacity  = Q
 //   dmean2D.x = -o (a Qx + b Qy) W/2,   dmean2D.y = -o (c Qy + b Qx) H/2
 //   dconic    = -o/2 (Qxx, Qxy, Qyy)    for conic (a, b, c), opacity o.
-__global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_inputs in,
+#ifdef GSR_GBWD_WAVES  // (A/B: a minimum waves-per-SIMD for the register allocator)
+#define GSR_GBWD_ATTR __attribute__((amdgpu_waves_per_eu(GSR_GBWD_WAVES)))
+#else
+#define GSR_GBWD_ATTR
+#endif
+__global__ void __launch_bounds__(256) GSR_GBWD_ATTR k_gaussian_backward(gsr_settings s, gsr_inputs in,
                                                            const int* __restrict__ radii,
                                                            const uint32_t* __restrict__ tiles_touched,
                                                            const uint32_t* __restrict__ goff,
+                                                           const uint32_t* __restrict__ bbase,
                                                            const uint8_t* __restrict__ clamped,
                                                            const float* __restrict__ contrib,
                                                            const uint8_t* __restrict__ written,
@@ -618,6 +736,14 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
     const int M = s.M;
     const size_t i3 = 3 * (size_t)idx;
     const bool live = idx < s.P;
+    // per-wave LDS: the record gather's, then the dsh staging's (each wave uses only its own part,
+    // so the two phases may share it without a block barrier): 21.5 KB per block, which leaves the
+    // kernel at its VGPR-bound occupancy
+    union WaveLds {
+        GatherLds g;
+        float4 srow[16][13];
+    };
+    __shared__ WaveLds s_wave[4];
     // Every per-Gaussian input that does not depend on the record sums is loaded up front
     // (clamped index for the tail threads), so that their latencies overlap each other
     // and the record gather instead of forming a chain of round trips after it.
@@ -626,7 +752,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
     Cam cam;
     load_cam_smem(s, cam);
     const int rad = radii[ci];
-    const uint32_t lo_slot = goff[ci], n_slot = tiles_touched[ci];
+    const uint32_t lo_slot = goff[ci] + bbase[ci / SLOT_BLOCK], n_slot = tiles_touched[ci];
     const float op = opac[ci];
     const f3 mean = ld3(in.means3D + c3i);
     float c3[6];
@@ -674,11 +800,17 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         if (g.drot && in.scales) for (int i = 0; i < 4; ++i) g.drot[4 * (size_t)idx + i] = 0.f;
         if (g.dsegments) { g.dsegments[2 * (size_t)idx] = 0.f; g.dsegments[2 * (size_t)idx + 1] = 0.f; }
     }
+    // gather-sum of the written instance records of the Gaussian's slot range
+    // [lo_slot, lo_slot + tiles_touched), in slot order (deterministic)
+    float q[12];
+#ifndef GSR_GATHER_PER_LANE
+    {
+        wave_gather(contrib, written, lo_slot, vis ? n_slot : 0u, q, s_wave[threadIdx.x >> 6].g);
+    }
+#else
+    if (vis) sum_records(contrib, written, lo_slot, lo_slot + n_slot, q);
+#endif
     if (vis) {
-        // gather-sum of the written instance records of the Gaussian's slot range
-        // [goff, goff + tiles_touched), in slot order (deterministic).
-        float q[12];
-        sum_records(contrib, written, lo_slot, lo_slot + n_slot, q);
         // the conic weighting of the mean2D channels happened per lane in the render backward
         const float dm2x = -op * q[7] * (0.5f * s.W);  // q[7] = sum q (a dx + b dy)
         const float dm2y = -op * q[8] * (0.5f * s.H);  // q[8] = sum q (b dx + c dy)
@@ -871,14 +1003,13 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
         // pass p: lanes 16p..16p+15 of each wave park their rows (padded to 52 floats:
         // conflict-free ds_write_b128), then the wave stores those 16 rows = 3 KB as
         // 192 consecutive float4s.
-        __shared__ float4 srow[4][16][13];
         const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
         const int wbase = blockIdx.x * blockDim.x + wave * 64;
         auto val = [&](int f) { return bas[f / 3] * dc[f % 3]; };
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             if ((lane >> 4) == p) {
-                float4* row = srow[wave][lane & 15];
+                float4* row = s_wave[wave].srow[lane & 15];
 #pragma unroll
                 for (int i = 0; i < 12; ++i)
                     row[i] = make_float4(val(4 * i), val(4 * i + 1), val(4 * i + 2), val(4 * i + 3));
@@ -890,7 +1021,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward(gsr_settings s, gsr_i
             for (int r = 0; r < 3; ++r) {
                 const int f = lane + 64 * r;  // float4 index in the 16-row run
                 const int row = f / 12, col = f - 12 * (f / 12);
-                if (g0 + row < s.P) sh_st(dst + f, srow[wave][row][col]);
+                if (g0 + row < s.P) sh_st(dst + f, s_wave[wave].srow[row][col]);
             }
             GSR_WAVE_SYNC();
         }
@@ -951,7 +1082,8 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int D, int 
         }
         const float op = w.opac[idx];
         float q[12];
-        sum_records(w.contrib, w.written, w.goff[idx], w.goff[idx] + w.tiles_touched[idx], q);
+        const uint32_t lo = w.goff[idx] + w.bbase[idx / SLOT_BLOCK];
+        sum_records(w.contrib, w.written, lo, lo + w.tiles_touched[idx], q);
         const float dm2x = -op * q[7] * (0.5f * w.W);  // q[7] = sum q (a dx + b dy)
         const float dm2y = -op * q[8] * (0.5f * w.H);  // q[8] = sum q (b dx + c dy)
         if (w.dmeans2D) { w.dmeans2D[i3] = dm2x; w.dmeans2D[i3 + 1] = dm2y; w.dmeans2D[i3 + 2] = 0.f; }
@@ -1189,12 +1321,12 @@ __global__ void __launch_bounds__(256) k_sh_dsh(int P, int D, int M, const float
 #if GSR_PRE_PART == 1
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec, int* radii,
                        uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped, ushort4* rect,
-                       uint32_t* rect32, float* shjac, float* opac, void* zero_a, size_t zero_a_bytes, void* zero_b,
-                       size_t zero_b_bytes, hipStream_t st) {
+                       uint32_t* rect32, float* shjac, float* opac, uint32_t* goff, uint32_t* btot, void* zero_a,
+                       size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes, hipStream_t st) {
     if (s.P == 0) return;
-    hipLaunchKernelGGL(k_preprocess, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, gx, gy, rec, radii,
-                       tiles_touched, depth_keys, clamped, rect, rect32, shjac, opac, zero_a, cdiv(zero_a_bytes, 16), zero_b,
-                       cdiv(zero_b_bytes, 16));
+    hipLaunchKernelGGL(k_preprocess, dim3(cdiv(s.P, SLOT_BLOCK)), dim3(SLOT_BLOCK), 0, st, s, in, gx, gy, rec, radii,
+                       tiles_touched, depth_keys, clamped, rect, rect32, shjac, opac, goff, btot, zero_a,
+                       cdiv(zero_a_bytes, 16), zero_b, cdiv(zero_b_bytes, 16));
 }
 
 void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t* present, hipStream_t st) {
@@ -1226,12 +1358,12 @@ void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const 
 
 #if GSR_PRE_PART == 2
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
-                              const uint32_t* tiles_touched, const uint32_t* goff, const uint8_t* clamped,
-                              const float* contrib, const uint8_t* written, const float* opac,
+                              const uint32_t* tiles_touched, const uint32_t* goff, const uint32_t* bbase,
+                              const uint8_t* clamped, const float* contrib, const uint8_t* written, const float* opac,
                               const float* shjac, const gsr_grads& g, float* shx, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_gaussian_backward, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, radii, tiles_touched,
-                       goff, clamped, contrib, written, opac, shjac, g, in.shs ? shx : nullptr);
+                       goff, bbase, clamped, contrib, written, opac, shjac, g, in.shs ? shx : nullptr);
 }
 
 #endif  // GSR_PRE_PART == 2

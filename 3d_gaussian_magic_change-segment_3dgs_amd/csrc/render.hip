@@ -215,22 +215,25 @@ __device__ __forceinline__ Batch fetch_batch(const float4* __restrict__ rec, uin
     const float4* R = rec + (size_t)g * REC_F4;
     return Batch{R[0], R[1], R[2]};
 }
-// The backward's batch fetch also takes the Gaussian's tile rectangle (record part 3, in the
-// 32-B sector of part 2) and its first record slot goff: the instance's slot is then
-// goff + (ty - y0) (x1 - x0) + (tx - x0) -- no per-instance slot array to read.
+// The backward's batch fetch also takes the Gaussian's tile rectangle and first record slot in its
+// block (record part 3, in the 32-B sector of part 2) and its block's slot base bbase[g / SLOT_BLOCK]
+// (gsr_internal.h): the instance's slot is then r.z + bb + (ty - y0) (x1 - x0) + (tx - x0) -- no
+// per-instance slot array to read.  The parts are added when the batch is used, not here: an add
+// at the fetch would wait for the prefetch loads.
 struct BatchB {
     float4 a, b, c;
-    uint2 r;
-    uint32_t go;
+    uint3 r;
+    uint32_t bb;
 };
-__device__ __forceinline__ BatchB fetch_batch_b(const float4* __restrict__ rec, const uint32_t* __restrict__ goff,
+__device__ __forceinline__ BatchB fetch_batch_b(const float4* __restrict__ rec, const uint32_t* __restrict__ bbase,
                                                 uint32_t g) {
     const float4* R = rec + (size_t)g * REC_F4;
-    return BatchB{R[0], R[1], R[2], *reinterpret_cast<const uint2*>(R + 3), goff[g]};
+    const uint4 r3 = *reinterpret_cast<const uint4*>(R + 3);
+    return BatchB{R[0], R[1], R[2], make_uint3(r3.x, r3.y, r3.z), bbase[g / SLOT_BLOCK]};
 }
 __device__ __forceinline__ uint32_t batch_slot(const BatchB& b, int tx, int ty) {
     const uint32_t x0 = b.r.x & 0xFFFFu, y0 = b.r.x >> 16, x1 = b.r.y & 0xFFFFu;
-    return b.go + ((uint32_t)ty - y0) * (x1 - x0) + ((uint32_t)tx - x0);
+    return b.r.z + b.bb + ((uint32_t)ty - y0) * (x1 - x0) + ((uint32_t)tx - x0);
 }
 
 // Lane-parallel batch prefilter: can ANY pixel centre of the tile rectangle
@@ -736,7 +739,7 @@ template <int NS, bool SPLIT>
 __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0, int wslot,
                                          const uint2* __restrict__ ranges,
                                          const uint32_t* __restrict__ point_list,
-                                         const uint32_t* __restrict__ goff,
+                                         const uint32_t* __restrict__ bbase,
                                          const float4* __restrict__ rec, const float* __restrict__ bg,
                                          const float* __restrict__ alphas,
                                          const uint32_t* __restrict__ n_contrib,
@@ -842,7 +845,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
     BatchB cur;
     if (top0 > 0) {
         g_next = plist[max(top0 - 1 - lane, 0)];
-        cur = fetch_batch_b(rec, goff, g_next);
+        cur = fetch_batch_b(rec, bbase, g_next);
     }
     if (top0 > 0) g_next = plist[max(top0 - 65 - lane, 0)];
     // Unsplit tiles park a batch's records in LDS (stage[j] = record of batch instance j) and
@@ -870,7 +873,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
             const int cnt = min(64, top - seg_lo);
             STAT(5, 1);
             flush();
-            const BatchB nxt = fetch_batch_b(rec, goff, g_next);
+            const BatchB nxt = fetch_batch_b(rec, bbase, g_next);
             g_next = plist[max(top - 129 - lane, 0)];
             const float4 ra = cur.a, rb = cur.b, rc = cur.c;
             const uint32_t uslot = batch_slot(cur, tx, ty);  // the instance's record slot
@@ -1092,7 +1095,7 @@ __device__ __forceinline__ uint32_t queue_tile(const TileSched& ts, int T, uint3
 
 __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k_render_bwd(
     int W, int H, int gx, int T, int split_depth, uint32_t* __restrict__ sched,
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ goff,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ bbase,
     const float4* __restrict__ rec, const float* __restrict__ bg, const float* __restrict__ alphas,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ dL_dsegs,
     const float* __restrict__ dL_ddepths, const float* __restrict__ dL_dalphas, float* __restrict__ contrib,
@@ -1120,11 +1123,11 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k
     // entry would be replayed whole, i.e. its records written twice with the same values
     const int tile = (int)(e & BQ_TILE);
     if (split) {
-        bwd_tile<2, true>(W, H, gx, tile, 2 * wid, (int)(2 * b + wid), ranges, point_list, goff, rec, bg,
+        bwd_tile<2, true>(W, H, gx, tile, 2 * wid, (int)(2 * b + wid), ranges, point_list, bbase, rec, bg,
                           alphas, n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written,
                           sh.srec[wid], &sh);
     } else {
-        bwd_tile<4, false>(W, H, gx, tile, 0, (int)(2 * b + wid), ranges, point_list, goff, rec, bg, alphas,
+        bwd_tile<4, false>(W, H, gx, tile, 0, (int)(2 * b + wid), ranges, point_list, bbase, rec, bg, alphas,
                            n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, sh.srec[wid],
                            nullptr, sh.stage[wid]);
     }
@@ -1140,7 +1143,7 @@ __global__ void __launch_bounds__(128) __attribute__((amdgpu_waves_per_eu(4))) k
 #endif
 __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD1_WAVES))) k_render_bwd1(
     int W, int H, int gx, int T, uint32_t* __restrict__ sched,
-    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ goff,
+    const uint2* __restrict__ ranges, const uint32_t* __restrict__ point_list, const uint32_t* __restrict__ bbase,
     const float4* __restrict__ rec, const float* __restrict__ bg, const float* __restrict__ alphas,
     const uint32_t* __restrict__ n_contrib, const float* __restrict__ dL_dpixels, const float* __restrict__ dL_dsegs,
     const float* __restrict__ dL_ddepths, const float* __restrict__ dL_dalphas, float* __restrict__ contrib,
@@ -1162,7 +1165,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD
     // a whole tile, or one of its list segments [0, ck) / [ck, depth) (publish_depth)
     const uint32_t kind = e & ~BQ_TILE;
     const int ck = (int)ts.sched[SCHED_CKPT];
-    bwd_tile<4, false>(W, H, gx, (int)(e & BQ_TILE), 0, (int)blockIdx.x, ranges, point_list, goff, rec,
+    bwd_tile<4, false>(W, H, gx, (int)(e & BQ_TILE), 0, (int)blockIdx.x, ranges, point_list, bbase, rec,
                        bg, alphas, n_contrib, dL_dpixels, dL_dsegs, dL_ddepths, dL_dalphas, contrib, written, srec,
                        nullptr, stage, kind == BQ_BACK ? ck : 0, kind == BQ_FRONT ? ck : 0x7fffffff,
                        kind == BQ_FRONT ? ckpt : nullptr);
@@ -1192,7 +1195,7 @@ void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, 
 
 #if GSR_RENDER_PART != 1
 void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
-                            const uint2* ranges, const uint32_t* point_list, const uint32_t* goff,
+                            const uint2* ranges, const uint32_t* point_list, const uint32_t* bbase,
                             const float4* rec, const float* bg, const float* alpha, const uint32_t* n_contrib,
                             const float* dL_dcolor, const float* dL_dsegment, const float* dL_ddepth,
                             const float* dL_dalpha, float* contrib, uint8_t* written, const float* ckpt,
@@ -1203,13 +1206,13 @@ void launch_render_backward(int W, int H, int gx, int gy, const uint32_t* order,
     if (split_bwd_depth() <= 0) {
         // up to two queue entries per tile (list segments); blocks past the queue return at once
         hipLaunchKernelGGL(k_render_bwd1, dim3(2 * T), dim3(64), 0, st, W, H, gx, T, sched, ranges, point_list,
-                           goff, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha,
+                           bbase, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha,
                            contrib, written, ckpt);
         return;
     }
     hipLaunchKernelGGL(k_render_bwd, dim3(T), dim3(128), 0, st, W, H, gx, T, split_bwd_depth(), sched, ranges,
                        point_list,
-                       goff, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib,
+                       bbase, rec, bg, alpha, n_contrib, dL_dcolor, dL_dsegment, dL_ddepth, dL_dalpha, contrib,
                        written);
 }
 
