@@ -885,6 +885,7 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
     else if (n == "order") G(GL.order, Pz * 4);
     else if (n == "goff") G(GL.goff, Pz * 4);
     else if (n == "bbase") G(GL.bbase, cdiv(Pz, (size_t)SLOT_BLOCK) * 4);
+    else if (n == "bbase") G(GL.bbase, cdiv(Pz, (size_t)SLOT_BLOCK) * 4);
     else if (n == "point_list") B(BL.point_list, I * 4);
     else if (n == "slot_vals") B(BL.slot_vals, I * 4);
     else if (n == "written") B(BL.written, I);  // the backward's written-record flags (1 byte per slot)

@@ -287,51 +287,69 @@ __device__ __forceinline__ uint32_t wave_or(uint32_t x) {
 __device__ __forceinline__ bool identity_pass(const uint32_t* span, int shift, int bits) {
     return (((span[0] & span[1]) >> shift) & ((1u << bits) - 1u)) == 0u;
 }
-// Record-slot block bases (gsr_internal.h SLOT_BLOCK): bbase[b] = sum of btot[0, b), b < nb, by one
-// block of HIST_THREADS threads: thread t scans a run of up to BB_RUN consecutive totals, all loaded
-// up front (one load latency per round of HIST_THREADS x BB_RUN totals, i.e. one round up to 2.1M
-// Gaussians), the runs' sums are scanned across the block.
-constexpr int BB_RUN = 8;
-__device__ void block_bases(const uint32_t* __restrict__ btot, uint32_t nb, uint32_t* __restrict__ bbase) {
+// Record-slot block bases (gsr_internal.h SLOT_BLOCK): bbase[b] = sum of btot[0, b), b < nb, in
+// segments of BB_SEG totals, segment k by block k of the histogram kernel (the blocks run
+// concurrently: one block doing every segment made the kernel ~9 us longer at C5).  Block k adds
+// up the totals before its segment (all loads up front) and scans its own (BB_RUN consecutive
+// totals per thread, the runs' sums scanned across the block).
+constexpr int BB_RUN = 8, BB_SEG = BB_RUN * HIST_THREADS;
+__device__ __forceinline__ uint32_t block_sum(uint32_t x, uint32_t* s_w) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) x += (uint32_t)__shfl_xor((int)x, o, 64);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = x;
+    __syncthreads();
+    uint32_t t = 0;
+#pragma unroll
+    for (int w = 0; w < HIST_THREADS / 64; ++w) t += s_w[w];
+    __syncthreads();
+    return t;
+}
+__device__ void block_bases(const uint32_t* __restrict__ btot, uint32_t nb, uint32_t* __restrict__ bbase, uint32_t seg) {
     __shared__ uint32_t s_w[HIST_THREADS / 64];
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    uint32_t carry = 0;
-    for (uint32_t r0 = 0; r0 < nb; r0 += BB_RUN * HIST_THREADS) {
-        const uint32_t per = min((uint32_t)BB_RUN, (nb - r0 + HIST_THREADS - 1) / HIST_THREADS);  // uniform
-        const uint32_t i0 = r0 + per * threadIdx.x;
-        uint32_t v[BB_RUN], s = 0;
+    const uint32_t r0 = seg * BB_SEG;
+    // totals before the segment: up to 8 per thread per round, loaded together
+    uint32_t pre_sum = 0;
+    for (uint32_t c0 = 0; c0 < r0; c0 += BB_SEG) {
+        uint32_t a[BB_RUN];
 #pragma unroll
         for (int k = 0; k < BB_RUN; ++k) {
-            v[k] = (uint32_t)k < per && i0 + k < nb ? btot[i0 + k] : 0u;
-            s += v[k];
+            const uint32_t i = c0 + (uint32_t)k * HIST_THREADS + threadIdx.x;
+            a[k] = i < r0 ? btot[i] : 0u;
         }
-        uint32_t x = s;
 #pragma unroll
-        for (int o = 1; o < 64; o <<= 1) {
-            const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
-            if (lane >= o) x += y;
-        }
-        if (lane == 63) s_w[wid] = x;
-        __syncthreads();
-        uint32_t pre = carry, tot = 0;
+        for (int k = 0; k < BB_RUN; ++k) pre_sum += a[k];
+    }
+    const uint32_t carry = r0 ? block_sum(pre_sum, s_w) : 0u;
+    const uint32_t i0 = r0 + BB_RUN * threadIdx.x;
+    uint32_t v[BB_RUN], s = 0;
 #pragma unroll
-        for (int w = 0; w < HIST_THREADS / 64; ++w) {
-            pre += w < wid ? s_w[w] : 0u;
-            tot += s_w[w];
-        }
-        __syncthreads();  // s_w is reused by the next round
-        pre += x - s;
+    for (int k = 0; k < BB_RUN; ++k) {
+        v[k] = i0 + k < nb ? btot[i0 + k] : 0u;
+        s += v[k];
+    }
+    uint32_t x = s;
 #pragma unroll
-        for (int k = 0; k < BB_RUN; ++k) {
-            if ((uint32_t)k < per && i0 + k < nb) bbase[i0 + k] = pre;
-            pre += v[k];
-        }
-        carry += tot;
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, o, 64);
+        if (lane >= o) x += y;
+    }
+    if (lane == 63) s_w[wid] = x;
+    __syncthreads();
+    uint32_t pre = carry;
+#pragma unroll
+    for (int w = 0; w < HIST_THREADS / 64; ++w) pre += w < wid ? s_w[w] : 0u;
+    pre += x - s;
+#pragma unroll
+    for (int k = 0; k < BB_RUN; ++k) {
+        if (i0 + k < nb) bbase[i0 + k] = pre;
+        pre += v[k];
     }
 }
+inline uint32_t block_base_segments(uint32_t nb) { return (nb + BB_SEG - 1) / BB_SEG; }
 __global__ void __launch_bounds__(HIST_THREADS) k_block_bases(const uint32_t* __restrict__ btot, uint32_t nb,
                                                               uint32_t* __restrict__ bbase) {
-    block_bases(btot, nb, bbase);
+    block_bases(btot, nb, bbase, blockIdx.x);
 }
 
 template <int HIST_ITEMS>
@@ -427,7 +445,7 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
         for (int p = 0; p < passes; ++p)
             if (cnt[p][threadIdx.x]) atomicAdd(&hist[p * RADIX + threadIdx.x], cnt[p][threadIdx.x]);
     if (threadIdx.x < 2 && s_span[threadIdx.x]) atomicOr(&span[threadIdx.x], s_span[threadIdx.x]);
-    if (bb_base && blockIdx.x == 0) block_bases(bb_tot, bb_n, bb_base);  // block-uniform
+    if (bb_base && blockIdx.x * BB_SEG < bb_n) block_bases(bb_tot, bb_n, bb_base, blockIdx.x);  // block-uniform
 #ifdef GSR_SORT_TRACE
     __syncthreads();
     if (threadIdx.x == 0 && blockIdx.x < 1024) {
@@ -1161,6 +1179,9 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
                      (keys_out != keys_in || (final_out && final_out->no_keys));
     const bool tally = (lb || grp) && final_out && final_out->tally && final_out->tally_host && !n_dev;
     if (final_out && final_out->tally_used) *final_out->tally_used = tally;
+    const bool bb = final_out && final_out->bb_base && final_out->bb_n;  // record-slot block bases
+    const bool bb_in_hist = bb && (lb || grp) &&
+                            cdiv(n, (size_t)HIST_THREADS * hist_items(n)) >= block_base_segments(final_out->bb_n);
     if (lb || grp) {
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_zero_bytes(n, passes), st);
@@ -1170,11 +1191,13 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
                            n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel, n_dev,
                            tally ? final_out->tally : nullptr,
                            reinterpret_cast<unsigned long long*>(W.counter + TALLY_WORD),
-                           final_out ? final_out->tally_host : nullptr, final_out ? final_out->bb_tot : nullptr,
-                           final_out ? final_out->bb_n : 0u, final_out ? final_out->bb_base : nullptr);
-    } else if (final_out && final_out->bb_base && final_out->bb_n) {
-        hipLaunchKernelGGL(k_block_bases, dim3(1), dim3(HIST_THREADS), 0, st, final_out->bb_tot, final_out->bb_n,
-                           final_out->bb_base);
+                           final_out ? final_out->tally_host : nullptr, bb_in_hist ? final_out->bb_tot : nullptr,
+                           bb_in_hist ? final_out->bb_n : 0u, bb_in_hist ? final_out->bb_base : nullptr);
+    }
+    if (bb && !bb_in_hist) {
+        // no histogram kernel, or fewer of its blocks than segments: the bases on their own
+        hipLaunchKernelGGL(k_block_bases, dim3(block_base_segments(final_out->bb_n)), dim3(HIST_THREADS), 0, st,
+                           final_out->bb_tot, final_out->bb_n, final_out->bb_base);
     }
     if (grp) {
         // grouped look-back passes with the pass plan on the device (k_radix_scatter_grp)

@@ -427,7 +427,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     if (lane == 63) s_wtot[wave] = t_incl;
     auto slot_scan_finish = [&]() {
         wave_lds_fence();
-        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_s_barrier();  // (without it: the same time, round5_h_index_order_slots.txt)
         wave_lds_fence();
         uint32_t pre = 0;
 #pragma unroll
@@ -1053,20 +1053,23 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int D, int 
         const float* cp = a.v[idx].campos;
         c[0] = cp[0]; c[1] = cp[1]; c[2] = cp[2]; c[3] = 0.f;
     }
-    if (idx >= P) return;
-    const size_t i3 = 3 * (size_t)idx;
-    const f3 mean = ld3(in.means3D + i3);
+    // no early exit: the per-view record gathers are wave operations (wave_gather)
+    const bool live = idx < P;
+    const int ci = live ? idx : 0;
+    const size_t i3 = 3 * (size_t)idx, c3i = 3 * (size_t)ci;
+    const f3 mean = ld3(in.means3D + c3i);
     float c3[6];
     float4 quat = make_float4(0.f, 0.f, 0.f, 0.f);
     f3 scale = {0.f, 0.f, 0.f};
     if (in.cov3D_precomp) {
 #pragma unroll
-        for (int i = 0; i < 6; ++i) c3[i] = in.cov3D_precomp[6 * (size_t)idx + i];
+        for (int i = 0; i < 6; ++i) c3[i] = in.cov3D_precomp[6 * (size_t)ci + i];
     } else {
-        quat = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)idx);
-        scale = ld3(in.scales + i3);
+        quat = *reinterpret_cast<const float4*>(in.rotations + 4 * (size_t)ci);
+        scale = ld3(in.scales + c3i);
         cov3d_from(scale, scale_modifier, quat, c3);
     }
+    __shared__ GatherLds s_gl[SLOT_BLOCK / 64];
     const M3 Vrk = vrk_of(c3);
     const auto& V = Vrk.m;
     f3 dmean_sum = {0.f, 0.f, 0.f}, dcol = {0.f, 0.f, 0.f};
@@ -1074,16 +1077,17 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int D, int 
     float dop = 0.f, dseg0 = 0.f, dseg1 = 0.f;
     for (int v = 0; v < a.B; ++v) {  // uniform: the view's fields are scalar loads
         const MvView& w = a.v[v];
-        float* drgb_v = shx ? shx + (size_t)v * chunk + i3 : nullptr;
-        if (!(w.radii[idx] > 0)) {
-            if (w.dmeans2D) { w.dmeans2D[i3] = 0.f; w.dmeans2D[i3 + 1] = 0.f; w.dmeans2D[i3 + 2] = 0.f; }
+        float* drgb_v = shx && live ? shx + (size_t)v * chunk + i3 : nullptr;
+        const bool vis_v = live && w.radii[ci] > 0;
+        float q[12];
+        wave_gather(w.contrib, w.written, w.goff[ci] + w.bbase[ci / SLOT_BLOCK], vis_v ? w.tiles_touched[ci] : 0u, q,
+                    s_gl[threadIdx.x >> 6]);
+        if (!vis_v) {
+            if (live && w.dmeans2D) { w.dmeans2D[i3] = 0.f; w.dmeans2D[i3 + 1] = 0.f; w.dmeans2D[i3 + 2] = 0.f; }
             if (drgb_v) { drgb_v[0] = 0.f; drgb_v[1] = 0.f; drgb_v[2] = 0.f; }
             continue;
         }
         const float op = w.opac[idx];
-        float q[12];
-        const uint32_t lo = w.goff[idx] + w.bbase[idx / SLOT_BLOCK];
-        sum_records(w.contrib, w.written, lo, lo + w.tiles_touched[idx], q);
         const float dm2x = -op * q[7] * (0.5f * w.W);  // q[7] = sum q (a dx + b dy)
         const float dm2y = -op * q[8] * (0.5f * w.H);  // q[8] = sum q (b dx + c dy)
         if (w.dmeans2D) { w.dmeans2D[i3] = dm2x; w.dmeans2D[i3 + 1] = dm2y; w.dmeans2D[i3 + 2] = 0.f; }
@@ -1194,6 +1198,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int D, int 
         }
         dmean_sum = dmean_sum + dmean;
     }
+    if (!live) return;
     if (g.dcolors) { g.dcolors[i3] = dcol.x; g.dcolors[i3 + 1] = dcol.y; g.dcolors[i3 + 2] = dcol.z; }
     if (g.dopacity) g.dopacity[idx] = dop;
     if (g.dsegments) { g.dsegments[2 * (size_t)idx] = dseg0; g.dsegments[2 * (size_t)idx + 1] = dseg1; }

@@ -152,7 +152,8 @@ EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_binning_capacity
 
 _DEBUG_FIELDS = {  # name -> (dtype, elements per unit, unit: P | I | T)
     "tiles_touched": (torch.int32, 1, "P"), "rec": (torch.float32, 16, "P"), "clamped": (torch.uint8, 1, "P"),
-    "order": (torch.int32, 1, "P"), "goff": (torch.int32, 1, "P"), "point_list": (torch.int32, 1, "I"),
+    "order": (torch.int32, 1, "P"), "goff": (torch.int32, 1, "P"), "bbase": (torch.int32, 1, "P/256"),
+    "point_list": (torch.int32, 1, "I"),
     "slot_vals": (torch.int32, 1, "I"), "ranges": (torch.int32, 2, "T"), "n_contrib_tiles": (torch.int32, 256, "T"),
     "written": (torch.uint8, 1, "I"),  # after a backward: 1 where the render backward stored a record
     "tile_order": (torch.int32, 1, "T+"),  # heavy-first tile order + the render schedule (gsr_internal.h TileSched)
@@ -170,7 +171,7 @@ def debug_state(name, P, W, H, num_rendered, geomBuffer, binningBuffer, imgBuffe
             raise RuntimeError(f"gsr_debug_copy({name}) size query failed: {_lib.gsr_last_error().decode()}")
         n = nb // 4
     else:
-        n = {"P": P, "I": num_rendered, "T": T}[unit] * per
+        n = {"P": P, "P/256": (P + 255) // 256, "I": num_rendered, "T": T}[unit] * per
     dev = geomBuffer.device
     out = torch.empty(max(n, 1), dtype=dtype, device=dev)
     ptr = lambda t: t.data_ptr() if t is not None and t.numel() else None

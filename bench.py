@@ -124,12 +124,13 @@ def algorithmic_bytes(stage, P, I, HW, deg, views=1, T=0, written=None):
         # the fused kernel's own minimal bytes (SURVEY's a14 + a15 + a16 figure,
         # (299 + 24 M) B, assumes separate launches that re-read the SH rows and pass dL_dmean3D /
         # dL_dcov3D through memory, and came out above the copy rate at 6M Gaussians).  Per
-        # Gaussian and view: radii, goff, tiles_touched, the 32-B half record, means3D, rotation,
-        # scale, clamp byte and the 36-B SH direction Jacobian read (121 B); dmeans2D, dopacity,
-        # dmeans3D, dscales, drot, dsegments and the 12 M-float dsh row written (64 + 12 M B).
-        # Per instance: its written flag (1 B); per written record: 48 B (W, measured).
+        # Gaussian and view: radii, tiles_touched, the in-block slot offset, opacity, means3D, rotation,
+        # scale, clamp byte and the 36-B SH direction Jacobian read (93 B; round 5: the opacity copy
+        # replaced the 32-B half record); dmeans2D, dopacity, dmeans3D,
+        # dscales, drot, dsegments and the 12 M-float dsh row written (64 + 12 M B).  Per
+        # instance: its written flag (1 B); per written record: 48 B (W, measured).
         W = written if written is not None else I
-        return ((121 + 64 + 12 * M) * P + I + 48 * W) * views
+        return ((93 + 64 + 12 * M) * P + I + 48 * W) * views
     return 0
 
 

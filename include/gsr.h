@@ -273,7 +273,9 @@ GSR_API int gsr_mark_visible(int P, const float* means3D, const float* viewmatri
  * forward call into dst (device memory; stream-ordered).  Names and element
  * types: "tiles_touched" u32[P], "rec" f32[P,16] ({x,y,conic.xyz,opacity,depth,
  * seg0,r,g,b,seg1,0...}), "clamped" u8[P], "order" u32[P] (depth order),
- * "goff" u32[P], "point_list" u32[I], "slot_vals" u32[I], "ranges" u32[T,2],
+ * "goff" u32[P] (the Gaussian's first record slot inside its block of 256 Gaussians: slots are
+ * numbered in Gaussian-index order), "bbase" u32[ceil(P/256)] (the slots before each block),
+ * "point_list" u32[I], "slot_vals" u32[I], "ranges" u32[T,2],
  * "n_contrib_tiles" u32[T,256] (tile-major, in the forward's 8x8-quadrant layout:
  * entry k*64+l of tile (tx, ty) is pixel (16*tx + 8*(k&1) + (l&7), 16*ty + 8*(k>>1) + (l>>3)),
  * k = 0..3 the quadrant, l = 0..63 the lane), "written" u8[I] (after a backward: 1 at

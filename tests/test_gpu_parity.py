@@ -291,8 +291,9 @@ def test_grid_wider_than_packed_rect(gpu_available, oracle_mod):
 def test_rows_binning_matches_radix_path(gpu_available, case):
     """binning_rows.hip (row-then-tile expansion, the default for grids <= 255 x 255
     tiles) and binning.hip's duplicate + radix tile sort build the same tile lists:
-    point_list, goff (every record slot is goff + the tile's place in the Gaussian's rectangle),
-    ranges, n_contrib, images and gradients bit for bit."""
+    point_list, ranges, n_contrib, images and gradients bit for bit.  Record slots follow the
+    Gaussian-index order in both (gsr_internal.h SLOT_BLOCK): goff is the exclusive scan of the
+    tile counts inside each block of 256 Gaussians, bbase that of the blocks' totals."""
     from diff_gaussian_rasterization import _C
     if case == "mt_small":
         scene, cam = synthetic_scene(60000, sh_degree=3, seed=41), orbit_camera(2, 640, 360, 400.0)
@@ -328,8 +329,16 @@ def test_rows_binning_matches_radix_path(gpu_available, case):
         assert int((edge[..., 1] > edge[..., 0]).sum()) > 0, "no Gaussian reaches the 255th tile row / column"
     for k in ("point_list", "ranges", "n_contrib", "color", "depth", "alpha", "segment", "radii"):
         np.testing.assert_array_equal(a[k], b[k], err_msg=k)
-    vis = a["radii"] > 0  # the row path writes goff for visible Gaussians only
-    np.testing.assert_array_equal(a["goff"][vis], b["goff"][vis], err_msg="goff")
+    tt = a["tiles_touched"].astype(np.int64)
+    blk_starts = np.arange(0, tt.size, 256)
+    blk = np.add.reduceat(tt, blk_starts)
+    want_bbase = np.concatenate([[0], np.cumsum(blk)[:-1]])
+    excl = np.cumsum(tt) - tt
+    want_goff = excl - np.repeat(excl[blk_starts], np.diff(np.append(blk_starts, tt.size)))
+    for r in (a, b):
+        np.testing.assert_array_equal(r["bbase"].astype(np.int64), want_bbase, err_msg="bbase")
+        np.testing.assert_array_equal(r["goff"].astype(np.int64), want_goff, err_msg="goff")
+    assert int(blk.sum()) == a["num_rendered"]
     for k in ga:
         np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
 
