@@ -1043,6 +1043,8 @@ __global__ void __launch_bounds__(256) GSR_GBWD_ATTR k_gaussian_backward(gsr_set
 //    and the rows (the SH exchange's rebuild after an all-gather of the rows, or the
 //    local batch), stored once through LDS as coalesced runs.
 // The shared inputs are read and the parameter gradients written once per batch.
+// (130 VGPRs, 3 waves/SIMD; a 4-wave hint fits 128 without spills but measured slower: 439 vs 423 us
+// per 8-view batch; 5 waves spill, 643 us -- profiles/round5_p_mv_occupancy.txt)
 __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int D, int M, float scale_modifier,
                                                               gsr_inputs in, MvArgs a, gsr_grads g,
                                                               float* __restrict__ shx) {
