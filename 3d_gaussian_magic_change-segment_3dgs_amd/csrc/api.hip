@@ -158,25 +158,40 @@ struct HostSlot {
     uint32_t* host = nullptr;  // CPU view
     uint32_t* dev = nullptr;   // GPU view of the same pinned word
 };
-HostSlot host_total_slot() {
-    thread_local HostSlot slot;
+// One word per call in flight: slot 0 for the calls that wait before returning, slots
+// 1..HOST_SLOTS-1 for gsr_forward_deferred calls (a ticket each until gsr_forward_wait).  The
+// calls of one host thread select their slot through t_slot.
+constexpr int HOST_SLOTS = 1 + GSR_MAX_DEFERRED;
+thread_local int t_slot = 0;
+struct HostSlots {
+    uint32_t* host = nullptr;
+    uint32_t* dev = nullptr;
+    bool busy[HOST_SLOTS] = {};
+};
+HostSlots& host_slots() {
+    thread_local HostSlots hs;
     thread_local bool tried = false;
     if (!tried) {
         tried = true;
         const char* env = getenv("GSR_HOST_TOTAL");
-        if (env && env[0] == '0') return slot;
+        if (env && env[0] == '0') return hs;
         void* p = nullptr;
         void* d = nullptr;
-        if (hipHostMalloc(&p, 64, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
+        if (hipHostMalloc(&p, 64 * HOST_SLOTS, hipHostMallocMapped | hipHostMallocCoherent) == hipSuccess) {
             if (hipHostGetDevicePointer(&d, p, 0) == hipSuccess) {
-                slot.host = (uint32_t*)p;
-                slot.dev = (uint32_t*)d;
+                hs.host = (uint32_t*)p;
+                hs.dev = (uint32_t*)d;
             } else {
                 (void)hipHostFree(p);
             }
         }
     }
-    return slot;
+    return hs;
+}
+HostSlot host_total_slot() {  // the current call's word (64 B apart: one cache line each)
+    HostSlots& hs = host_slots();
+    if (!hs.host) return HostSlot{};
+    return HostSlot{hs.host + 16 * t_slot, hs.dev + 16 * t_slot};
 }
 int wait_total(uint32_t* hslot, hipStream_t st, const uint32_t* dev_last, uint32_t* total) {
     if (hslot) {
@@ -535,6 +550,53 @@ int render_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, void* b
     return 0;
 }
 }  // namespace
+
+int gsr_forward_deferred(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* binning,
+                         size_t binning_bytes, void* img, float* out_color, float* out_depth, float* out_alpha,
+                         float* out_segment, void* stream, int* ticket) {
+    using namespace gsr;
+    g_last_error.clear();
+    if (!ticket) return fail("[gsr] forward_deferred: ticket is NULL");
+    *ticket = -1;
+    const size_t C = s && s->binning_capacity > 0 ? (size_t)s->binning_capacity : 0;
+    if (!s || s->P <= 0 || C == 0 || !binning || gsr_binning_bytes((int)C) > binning_bytes)
+        return fail("[gsr] forward_deferred: needs P > 0 and a binning buffer laid out for binning_capacity > 0");
+    HostSlots& hs = host_slots();
+    int k = 1;
+    while (k < HOST_SLOTS && hs.busy[k]) ++k;
+    if (k == HOST_SLOTS) return fail("[gsr] forward_deferred: too many calls in flight (gsr_forward_wait each)");
+    t_slot = k;
+    int nr = 0;
+    int rc = geometry_impl(s, in, geom, radii, stream, &nr, false);
+    if (rc == 0) {
+        const GeomLayout L = geom_layout((size_t)s->P);
+        const uint32_t* n_dev = at<uint32_t>(aligned_base(geom), L.offsets) + (s->P - 1);
+        rc = render_impl(s, in, geom, binning, img, C, C, n_dev, out_color, out_depth, out_alpha, out_segment,
+                         stream);
+    }
+    t_slot = 0;
+    if (rc) return rc;
+    hs.busy[k] = true;
+    *ticket = k;
+    return 0;
+}
+
+int gsr_forward_wait(int ticket, const gsr_settings* s, const void* geom, void* stream, int* num_rendered) {
+    using namespace gsr;
+    g_last_error.clear();
+    if (ticket < 1 || ticket >= HOST_SLOTS) return fail("[gsr] forward_wait: not a pending ticket");
+    HostSlots& hs = host_slots();
+    if (!hs.busy[ticket]) return fail("[gsr] forward_wait: not a pending ticket");
+    hs.busy[ticket] = false;
+    if (!s || !geom || !num_rendered || s->P <= 0) return fail("[gsr] forward_wait: null argument");
+    const GeomLayout L = geom_layout((size_t)s->P);
+    const uint32_t* n_dev = at<uint32_t>(aligned_base(const_cast<void*>(geom)), L.offsets) + (s->P - 1);
+    uint32_t total = 0;
+    if (int rc = wait_total(hs.host ? hs.host + 16 * ticket : nullptr, (hipStream_t)stream, n_dev, &total)) return rc;
+    if (total > 0x7FFFFFFFu) return fail("[gsr] num_rendered overflows int32");
+    *num_rendered = (int)total;
+    return total > (uint32_t)s->binning_capacity ? GSR_NEED_BINNING : 0;
+}
 
 int gsr_forward(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii, void* binning,
                 size_t binning_bytes, void* img, float* out_color, float* out_depth, float* out_alpha,

@@ -68,6 +68,11 @@ _lib.gsr_forward.restype = _i
 _lib.gsr_forward.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _vp, _vp, _vp, _sz, _vp,
                              _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_int)]
 GSR_NEED_BINNING = 2
+_lib.gsr_forward_deferred.restype = _i
+_lib.gsr_forward_deferred.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _vp, _vp, _vp, _sz, _vp,
+                                      _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(ctypes.c_int)]
+_lib.gsr_forward_wait.restype = _i
+_lib.gsr_forward_wait.argtypes = [_i, ctypes.POINTER(_Settings), _vp, _vp, ctypes.POINTER(ctypes.c_int)]
 _lib.gsr_backward.restype = _i
 _lib.gsr_backward.argtypes = [ctypes.POINTER(_Settings), ctypes.POINTER(_Inputs), _vp, _vp, _vp, _vp, _i, _vp,
                               _vp, _vp, _vp, _vp, _vp, ctypes.POINTER(_Grads), _vp]
@@ -141,7 +146,8 @@ if hasattr(_lib, "gsr_dp_init"):
     _lib.gsr_dp_wait.argtypes = [_i, _vp]
 
 EXPORTED_SYMBOLS = ("gsr_geom_bytes", "gsr_binning_bytes", "gsr_binning_capacity", "gsr_img_bytes", "gsr_backward_scratch_bytes",
-                    "gsr_forward_geometry", "gsr_forward_render", "gsr_forward", "gsr_backward", "gsr_mark_visible",
+                    "gsr_forward_geometry", "gsr_forward_render", "gsr_forward", "gsr_forward_deferred",
+                    "gsr_forward_wait", "gsr_backward", "gsr_mark_visible",
                     "gsr_debug_copy", "gsr_num_stages", "gsr_stage_name", "gsr_timing_enable", "gsr_timing_collect",
                     "gsr_stream_copy",
                     "gsr_last_error", "gsr_version", "gsr_set_option", "gsr_multiview_scratch_bytes",
@@ -260,6 +266,29 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
                         degree, campos, prefiltered, debug):
     """RasterizeGaussiansCUDA (DGR/rasterize_points.cu:35-125).
     Returns (num_rendered, color, depth, segment, alpha, radii, geomBuffer, binningBuffer, imgBuffer)."""
+    return rasterize_gaussians_end(_forward_begin(False, background, means3D, colors, segments, opacity, scales,
+                                                  rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
+                                                  tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
+                                                  prefiltered, debug))
+
+
+# GSR_MV_DEFERRED=0: rasterize_gaussians_begin waits like rasterize_gaussians (A/B of the deferred forward)
+_DEFERRED = os.environ.get("GSR_MV_DEFERRED", "1") != "0"
+
+
+def rasterize_gaussians_begin(*args):
+    """rasterize_gaussians split for a batch of views (same arguments): launches the view's
+    forward and returns a handle at once when a binning-capacity guess exists
+    (gsr_forward_deferred), so that the next views' launches do not wait for this view's
+    num_rendered; rasterize_gaussians_end(handle), called on the same stream, waits and returns
+    rasterize_gaussians' tuple.  Every handle must be ended (at most GSR_MAX_DEFERRED = 16
+    open per thread)."""
+    return _forward_begin(_DEFERRED, *args)
+
+
+def _forward_begin(deferred, background, means3D, colors, segments, opacity, scales, rotations, scale_modifier,
+                   cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh,
+                   degree, campos, prefiltered, debug):
     if means3D.dim() != 2 or means3D.size(1) != 3:
         raise RuntimeError("means3D must have dimensions (num_points, 3)")
     P, H, W = int(means3D.size(0)), int(image_height), int(image_width)
@@ -271,8 +300,9 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
         if P == 0:  # reference leaves the zero-filled outputs untouched (rasterize_points.cu:87)
             z = lambda *s: torch.zeros(*s, **f32)
             empty = torch.empty(0, dtype=torch.uint8, device=device)
-            return (0, z(NUM_CHANNELS, H, W), z(1, H, W), z(NUM_CLASS, H, W), z(1, H, W),
-                    torch.zeros(0, dtype=torch.int32, device=device), empty, empty.clone(), empty.clone())
+            return {"result": (0, z(NUM_CHANNELS, H, W), z(1, H, W), z(NUM_CLASS, H, W), z(1, H, W),
+                               torch.zeros(0, dtype=torch.int32, device=device), empty, empty.clone(),
+                               empty.clone())}
         means3D_ = _dev_f32(means3D, device, "means3D")
         sh_ = _dev_f32(sh, device, "sh")
         colors_ = _dev_f32(colors, device, "colors_precomp")
@@ -313,26 +343,58 @@ def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, 
         # every call on a binning buffer uses the layout of its capacity (gsr.h); with a guess
         # gsr_forward runs stage B speculatively right behind stage A
         s.binning_capacity = binning_capacity(binning)
+        h = {"s": s, "inp": inp, "stream": stream, "device": device, "geom": geom, "img": img, "radii": radii,
+             "color": color, "depth": depth, "alpha": alpha, "segment": segment, "binning": binning,
+             # the device inputs the launches read stay referenced until the handle is ended
+             "keep": (means3D_, sh_, colors_, segments_, opacity_, scales_, rotations_, cov_, bg_, view_, proj_,
+                      campos_)}
+        bptr = binning.data_ptr() if binning is not None else None
+        bbytes = binning.numel() if binning is not None else 0
+        if deferred and cap and not debug:
+            t = ctypes.c_int(-1)
+            _check(_lib.gsr_forward_deferred(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), radii.data_ptr(),
+                                             bptr, bbytes, img.data_ptr(), color.data_ptr(), depth.data_ptr(),
+                                             alpha.data_ptr(), segment.data_ptr(), stream, ctypes.byref(t)))
+            h["ticket"] = t.value
+            return h
         nr = ctypes.c_int(0)
         # geometry, the num_rendered sync and the render in one C call when the guess holds
-        rc = _lib.gsr_forward(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), radii.data_ptr(),
-                              binning.data_ptr() if binning is not None else None,
-                              binning.numel() if binning is not None else 0, img.data_ptr(), color.data_ptr(),
-                              depth.data_ptr(), alpha.data_ptr(), segment.data_ptr(), stream, ctypes.byref(nr))
-        num_rendered = int(nr.value)
+        h["rc"] = _lib.gsr_forward(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), radii.data_ptr(), bptr,
+                                   bbytes, img.data_ptr(), color.data_ptr(), depth.data_ptr(), alpha.data_ptr(),
+                                   segment.data_ptr(), stream, ctypes.byref(nr))
+        h["num_rendered"] = int(nr.value)
+        return h
+
+
+def rasterize_gaussians_end(h):
+    """Completes a rasterize_gaussians_begin handle (see there)."""
+    if "result" in h:
+        return h["result"]
+    s, device, stream = h["s"], h["device"], h["stream"]
+    with torch.cuda.device(device):
+        if "ticket" in h:
+            nr = ctypes.c_int(0)
+            rc = _lib.gsr_forward_wait(h.pop("ticket"), ctypes.byref(s), h["geom"].data_ptr(), stream,
+                                       ctypes.byref(nr))
+            num_rendered = int(nr.value)
+        else:
+            rc, num_rendered = h["rc"], h["num_rendered"]
         recent = _last_rendered.setdefault(device, [])
         recent.append(num_rendered)
         del recent[:-_GUESS_WINDOW]
+        binning = h["binning"]
         if rc == GSR_NEED_BINNING:  # no guess, or too small: stage B with the exact size
-            binning = torch.empty(_lib.gsr_binning_bytes(num_rendered), **u8)
+            binning = torch.empty(_lib.gsr_binning_bytes(num_rendered), dtype=torch.uint8, device=device)
             s.binning_capacity = binning_capacity(binning)
-            rc = _lib.gsr_forward_render(ctypes.byref(s), ctypes.byref(inp), geom.data_ptr(), binning.data_ptr(),
-                                         img.data_ptr(), num_rendered, color.data_ptr(), depth.data_ptr(),
-                                         alpha.data_ptr(), segment.data_ptr(), stream)
+            rc = _lib.gsr_forward_render(ctypes.byref(s), ctypes.byref(h["inp"]), h["geom"].data_ptr(),
+                                         binning.data_ptr(), h["img"].data_ptr(), num_rendered,
+                                         h["color"].data_ptr(), h["depth"].data_ptr(), h["alpha"].data_ptr(),
+                                         h["segment"].data_ptr(), stream)
         _check(rc)
         if binning is None:  # num_rendered == 0 with no guess
-            binning = torch.empty(0, **u8)
-    return num_rendered, color, depth, segment, alpha, radii, geom, binning, img
+            binning = torch.empty(0, dtype=torch.uint8, device=device)
+    return (num_rendered, h["color"], h["depth"], h["segment"], h["alpha"], h["radii"], h["geom"], binning,
+            h["img"])
 
 
 def set_option(name, value):

@@ -283,13 +283,33 @@ class _RasterizeGaussiansMultiview(torch.autograd.Function):
                                      and not any(rs.debug for rs in settings_list)) else None
         if side is not None:
             side.wait_stream(main)
+        # Every view's forward is launched before any view's num_rendered is waited for
+        # (rasterize_gaussians_begin / _end: gsr_forward_deferred), so that the host's launches
+        # are not gated on each view's binning: both streams stay fed.
+        handles = []
+        try:
+            for v, rs in enumerate(settings_list):
+                on_side = side is not None and (v & 1) == 1
+                with torch.cuda.stream(side) if on_side else contextlib.nullcontext():
+                    handles.append(_C.rasterize_gaussians_begin(
+                        rs.bg, means3D, colors_precomp, segments, opacities, scales, rotations, rs.scale_modifier,
+                        cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
+                        rs.image_width, sh, rs.sh_degree, rs.campos, rs.prefiltered, rs.debug))
+        except BaseException:
+            for v, h in enumerate(handles):  # every started forward is waited for (its ticket freed)
+                try:
+                    with torch.cuda.stream(side) if side is not None and (v & 1) == 1 else contextlib.nullcontext():
+                        _C.rasterize_gaussians_end(h)
+                except Exception:
+                    pass
+            if side is not None:
+                main.wait_stream(side)
+            raise
         for v, rs in enumerate(settings_list):
             on_side = side is not None and (v & 1) == 1
             with torch.cuda.stream(side) if on_side else contextlib.nullcontext():
-                out = _C.rasterize_gaussians(rs.bg, means3D, colors_precomp, segments, opacities, scales,
-                                             rotations, rs.scale_modifier, cov3Ds_precomp, rs.viewmatrix,
-                                             rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
-                                             rs.image_width, sh, rs.sh_degree, rs.campos, rs.prefiltered, rs.debug)
+                out = _C.rasterize_gaussians_end(handles[v])
+            handles[v] = None
             num_rendered, color, depth, segment, alpha, radii, geom, binning, img = out
             if on_side:
                 for t in (color, depth, segment, alpha, radii, geom, binning, img):

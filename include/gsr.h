@@ -155,6 +155,25 @@ GSR_API int gsr_forward(const gsr_settings* s, const gsr_inputs* in, void* geom,
                         size_t binning_bytes, void* img, float* out_color, float* out_depth, float* out_alpha,
                         float* out_segment, void* stream, int* num_rendered);
 
+/* ---- deferred forward (a multi-view batch): gsr_forward's speculative path (requires
+ * s->binning_capacity = C > 0 and binning_bytes >= gsr_binning_bytes(C)) split in two.
+ * gsr_forward_deferred launches stage A and stage B and returns at once with *ticket; the
+ * host can launch the next views meanwhile (gsr_forward waits for num_rendered before it
+ * returns, which gates the host's next launches on this view's binning).
+ * gsr_forward_wait(ticket, the same s, geom and stream) then waits for num_rendered:
+ * 0 (rendered), GSR_NEED_BINNING (num_rendered > C: stage B's outputs are void; call
+ * gsr_forward_render with a buffer of gsr_binning_bytes(*num_rendered)), or an error.
+ * Each host thread may hold up to GSR_MAX_DEFERRED tickets; every ticket must be waited
+ * for (once).  No counterpart in the reference (rasterize_points.cu:35-125 renders one
+ * view per call and syncs inside it). */
+#define GSR_MAX_DEFERRED 16
+GSR_API int gsr_forward_deferred(const gsr_settings* s, const gsr_inputs* in, void* geom, int* radii,
+                                 void* binning, size_t binning_bytes, void* img, float* out_color,
+                                 float* out_depth, float* out_alpha, float* out_segment, void* stream,
+                                 int* ticket);
+GSR_API int gsr_forward_wait(int ticket, const gsr_settings* s, const void* geom, void* stream,
+                             int* num_rendered);
+
 /* ---- backward.  Replaces Rasterizer::backward (rasterizer_impl.cu:348-458) /
  * RasterizeGaussiansBackwardCUDA (rasterize_points.cu:127-221).  dL_d* are the
  * upstream image gradients (same shapes as the forward outputs); alpha is the

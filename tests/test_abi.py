@@ -193,3 +193,20 @@ def test_native_exchange_reports_errors_before_init():
     assert b"not initialised" in L.gsr_last_error()
     for t in (-1, 0, 16):  # (the wait takes the lock and checks the communicator first)
         assert L.gsr_dp_wait(t, None) != 0 and b"not initialised" in L.gsr_last_error()
+
+
+def test_deferred_forward_validates_without_the_device():
+    """gsr_forward_deferred needs a binning buffer laid out for a capacity guess, and
+    gsr_forward_wait only accepts a pending ticket: both fail cleanly before any device work."""
+    from diff_gaussian_rasterization import _C
+    L = ctypes.CDLL(_C.LIB_PATH)
+    L.gsr_last_error.restype = ctypes.c_char_p
+    t = ctypes.c_int(5)
+    assert L.gsr_forward_deferred(None, None, None, None, None, ctypes.c_size_t(0), None, None, None, None, None,
+                                  None, ctypes.byref(t)) != 0
+    assert t.value == -1 and b"binning_capacity" in L.gsr_last_error()
+    nr = ctypes.c_int(0)
+    for bad in (0, -1, 999):
+        assert L.gsr_forward_wait(bad, None, None, None, ctypes.byref(nr)) != 0
+        assert b"not a pending ticket" in L.gsr_last_error()
+

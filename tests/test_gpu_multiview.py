@@ -262,3 +262,24 @@ def test_deferred_sh_single_view_completes_to_dropin(gpu_available):
     _C.sh_backward(rows, 1, means3D.detach(), sh.detach(), degree, dsh, dmeans3D)
     for k, a, b in zip(list(d) + ["means2D"], got, ref):
         assert torch.equal(a, b), f"{k} differs after the SH completion"
+
+
+def test_multiview_deferred_forward_rebinning(gpu_available):
+    """The multi-view forward launches every view before waiting for any num_rendered
+    (gsr_forward_deferred / gsr_forward_wait).  With a binning guess far below the views'
+    counts, every view takes gsr_forward_wait's GSR_NEED_BINNING path and re-runs stage B with
+    the exact buffer: outputs still equal the single-view drop-in's, bit for bit."""
+    from diff_gaussian_rasterization import _C, rasterize_gaussians
+    scene = synthetic_scene(20000, sh_degree=3, seed=47)
+    d = _leaves(scene)
+    views = _views(3, 3, W=320, H=240)
+    ref = [rasterize_gaussians(d["means3D"], torch.zeros_like(d["means3D"]), raster_settings=st, **_kw(d))
+           for st, _ in views]
+    assert all(int((r[1] > 0).sum()) > 0 for r in ref)
+    dev = d["means3D"].device
+    _C._last_rendered[dev] = [1]  # guess: 1 + 4096 instances, far below the counts
+    got, _, outs = _multi(d, views)
+    for o, r in zip(outs, ref):
+        for a, b in zip(o, r):
+            assert torch.equal(a, b)
+    assert max(_C._last_rendered[dev]) > 4097  # the counts were above the guess
