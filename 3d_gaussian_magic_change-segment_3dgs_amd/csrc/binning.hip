@@ -288,7 +288,7 @@ __device__ __forceinline__ bool identity_pass(const uint32_t* span, int shift, i
     return (((span[0] & span[1]) >> shift) & ((1u << bits) - 1u)) == 0u;
 }
 // Record-slot block bases (gsr_internal.h SLOT_BLOCK): bbase[b] = sum of btot[0, b), b < nb, in
-// segments of BB_SEG totals, segment k by block k of the histogram kernel (the blocks run
+// segments of BB_SEG totals, segment k by the histogram kernel's k-th extra block (the blocks run
 // concurrently: one block doing every segment made the kernel ~9 us longer at C5).  Block k adds
 // up the totals before its segment (all loads up front) and scans its own (BB_RUN consecutive
 // totals per thread, the runs' sums scanned across the block).
@@ -361,6 +361,13 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
                                                              unsigned long long* tally_word, uint32_t* tally_host,
                                                              const uint32_t* __restrict__ bb_tot, uint32_t bb_n,
                                                              uint32_t* __restrict__ bb_base) {
+    // the record-slot block bases run on extra blocks past the histogram's (beside them: a
+    // histogram block that also did them set the kernel's end, +3 us at the metric scene)
+    const uint32_t nseg = bb_base ? (bb_n + BB_SEG - 1) / BB_SEG : 0u, hblocks = gridDim.x - nseg;
+    if (blockIdx.x >= hblocks) {  // block-uniform
+        block_bases(bb_tot, bb_n, bb_base, blockIdx.x - hblocks);
+        return;
+    }
     ST_T(st0)
     if (n_dev) n = min(n, (size_t)*n_dev);
     __shared__ uint32_t cnt[4][RADIX];
@@ -436,7 +443,7 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
         const unsigned long long mine = (1ull << 40) | s_span[2];
         const unsigned long long old =
             __hip_atomic_fetch_add(tally_word, mine, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if ((old >> 40) + 1 == gridDim.x)
+        if ((old >> 40) + 1 == hblocks)
             __hip_atomic_store(tally_host, (uint32_t)((old + mine) & ((1ull << 40) - 1)), __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_SYSTEM);
     }
@@ -445,7 +452,6 @@ __global__ void __launch_bounds__(HIST_THREADS) k_radix_hist(const uint32_t* __r
         for (int p = 0; p < passes; ++p)
             if (cnt[p][threadIdx.x]) atomicAdd(&hist[p * RADIX + threadIdx.x], cnt[p][threadIdx.x]);
     if (threadIdx.x < 2 && s_span[threadIdx.x]) atomicOr(&span[threadIdx.x], s_span[threadIdx.x]);
-    if (bb_base && blockIdx.x * BB_SEG < bb_n) block_bases(bb_tot, bb_n, bb_base, blockIdx.x);  // block-uniform
 #ifdef GSR_SORT_TRACE
     __syncthreads();
     if (threadIdx.x == 0 && blockIdx.x < 1024) {
@@ -1180,14 +1186,14 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
     const bool tally = (lb || grp) && final_out && final_out->tally && final_out->tally_host && !n_dev;
     if (final_out && final_out->tally_used) *final_out->tally_used = tally;
     const bool bb = final_out && final_out->bb_base && final_out->bb_n;  // record-slot block bases
-    const bool bb_in_hist = bb && (lb || grp) &&
-                            cdiv(n, (size_t)HIST_THREADS * hist_items(n)) >= block_base_segments(final_out->bb_n);
+    const bool bb_in_hist = bb && (lb || grp);
     if (lb || grp) {
         const size_t nt = sort_tiles(n, sort_lb_items());
         if (!ws_zeroed) (void)hipMemsetAsync(W.base, 0, sort_zero_bytes(n, passes), st);
         const int hi = hist_items(n);
         auto hist_kern = hi == 4 ? k_radix_hist<4> : hi == 8 ? k_radix_hist<8> : k_radix_hist<16>;
-        hipLaunchKernelGGL(hist_kern, dim3((unsigned)cdiv(n, (size_t)HIST_THREADS * hi)), dim3(HIST_THREADS), 0, st, keys_in,
+        const size_t hblocks = cdiv(n, (size_t)HIST_THREADS * hi) + (bb_in_hist ? block_base_segments(final_out->bb_n) : 0);
+        hipLaunchKernelGGL(hist_kern, dim3((unsigned)hblocks), dim3(HIST_THREADS), 0, st, keys_in,
                            n, passes, per_pass, key_bits, W.hist, W.counter + SPAN_WORD, (int)skip_sentinel, n_dev,
                            tally ? final_out->tally : nullptr,
                            reinterpret_cast<unsigned long long*>(W.counter + TALLY_WORD),
@@ -1195,7 +1201,7 @@ void launch_radix_sort(const uint32_t* keys_in, const uint32_t* vals_in, uint32_
                            bb_in_hist ? final_out->bb_n : 0u, bb_in_hist ? final_out->bb_base : nullptr);
     }
     if (bb && !bb_in_hist) {
-        // no histogram kernel, or fewer of its blocks than segments: the bases on their own
+        // no histogram kernel: the bases on their own
         hipLaunchKernelGGL(k_block_bases, dim3(block_base_segments(final_out->bb_n)), dim3(HIST_THREADS), 0, st,
                            final_out->bb_tot, final_out->bb_n, final_out->bb_base);
     }
