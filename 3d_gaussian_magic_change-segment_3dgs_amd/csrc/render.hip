@@ -371,10 +371,6 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
     // kept as a wave mask in SGPRs (no per-pair VALU compare); T stays at its value at
     // termination, which is the T the output uses (forward.cu:355-357 breaks before T).
     float T[NQ], C0[NQ], C1[NQ], C2[NQ], S0[NQ], S1[NQ], Dp[NQ], Wt[NQ];
-#ifdef GSR_CK_REGS
-    // (A/B) the checkpoint's T and the sums before it stay in registers until the end transform
-    float kT[NQ], kC0[NQ], kC1[NQ], kC2[NQ], kS0[NQ], kS1[NQ], kDp[NQ];
-#endif
     uint32_t last[NQ];
     uint64_t live[NQ];
 #pragma unroll
@@ -418,14 +414,6 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
             // two parts added (the weight sum runs on: T_final = 1 - weight sum must stay the
             // reference's).  Wave-uniform base + 32-bit lane offsets (saddr stores: no per-lane
             // 64-bit addresses for the compiler to keep live across the loop).
-#ifdef GSR_CK_REGS
-#pragma unroll
-            for (int kk = 0; kk < NQ; ++kk) {
-                kT[kk] = T[kk]; kC0[kk] = C0[kk]; kC1[kk] = C1[kk]; kC2[kk] = C2[kk];
-                kS0[kk] = S0[kk]; kS1[kk] = S1[kk]; kDp[kk] = Dp[kk];
-                C0[kk] = C1[kk] = C2[kk] = S0[kk] = S1[kk] = Dp[kk] = 0.f;
-            }
-#else
             float* cp = ckpt + (size_t)__builtin_amdgcn_readfirstlane(tile) * CKPT_FLOATS;
 #pragma unroll
             for (int kk = 0; kk < NQ; ++kk) {
@@ -439,7 +427,6 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
                 cp[o + 6 * TILE_PIX] = Dp[kk];
                 C0[kk] = C1[kk] = C2[kk] = S0[kk] = S1[kk] = Dp[kk] = 0.f;
             }
-#endif
             wrote_ck = true;
         }
         const int cnt = min(64, n - base);
@@ -569,14 +556,9 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
 #pragma unroll
         for (int kk = 0; kk < NQ; ++kk) {
             const uint32_t o = 64u * (uint32_t)(q0 + kk) + (uint32_t)lane;
-#ifdef GSR_CK_REGS
-            const float Tc = kT[kk];
-            const float b0 = kC0[kk], b1 = kC1[kk], b2 = kC2[kk], b3 = kS0[kk], b4 = kS1[kk], b5 = kDp[kk];
-#else
             const float Tc = cp[o];
             const float b0 = cp[o + 1 * TILE_PIX], b1 = cp[o + 2 * TILE_PIX], b2 = cp[o + 3 * TILE_PIX];
             const float b3 = cp[o + 4 * TILE_PIX], b4 = cp[o + 5 * TILE_PIX], b5 = cp[o + 6 * TILE_PIX];
-#endif
             const float rT = 1.0f / Tc;  // T(ck) > 0: at least T_MIN * 0.01 on any pixel
             cp[o + 0 * TILE_PIX] = (1.0f - Wt[kk]) * (Tc / T[kk]);
             cp[o + 1 * TILE_PIX] = C0[kk] * rT;

@@ -73,11 +73,15 @@ _MV_STREAMS = os.environ.get("GSR_MV_STREAMS", "1") != "0"
 _VIEW_STREAMS = {}
 
 
-def _view_stream(device):
-    st = _VIEW_STREAMS.get(device)
-    if st is None:
-        st = _VIEW_STREAMS[device] = torch.cuda.Stream(device=device)
-    return st
+# streams the multi-view forward deals its views over (the caller's + MV_FWD_STREAMS - 1 side ones)
+_MV_FWD_STREAMS = max(2, int(os.environ.get("GSR_MV_FWD_STREAMS", "2")))
+
+
+def _view_streams(device, n):
+    sts = _VIEW_STREAMS.setdefault(device, [])
+    while len(sts) < n:
+        sts.append(torch.cuda.Stream(device=device))
+    return sts[:n]
 
 
 def _sh_sink():
@@ -279,18 +283,21 @@ class _RasterizeGaussiansMultiview(torch.autograd.Function):
         outs, views = [], []
         dev = means3D.device
         main = torch.cuda.current_stream(dev) if means3D.is_cuda else None
-        side = _view_stream(dev) if (main is not None and len(settings_list) > 1 and _MV_STREAMS
-                                     and not any(rs.debug for rs in settings_list)) else None
-        if side is not None:
-            side.wait_stream(main)
+        multi = (main is not None and len(settings_list) > 1 and _MV_STREAMS
+                 and not any(rs.debug for rs in settings_list))
+        # view v runs on stream v % K: the caller's (0) or a side stream
+        sides = _view_streams(dev, min(_MV_FWD_STREAMS, len(settings_list)) - 1) if multi else []
+        for sd in sides:
+            sd.wait_stream(main)
+        vstream = lambda v: sides[v % (len(sides) + 1) - 1] if sides and v % (len(sides) + 1) else None
         # Every view's forward is launched before any view's num_rendered is waited for
         # (rasterize_gaussians_begin / _end: gsr_forward_deferred), so that the host's launches
         # are not gated on each view's binning: both streams stay fed.
         handles = []
         try:
             for v, rs in enumerate(settings_list):
-                on_side = side is not None and (v & 1) == 1
-                with torch.cuda.stream(side) if on_side else contextlib.nullcontext():
+                sv = vstream(v)
+                with torch.cuda.stream(sv) if sv is not None else contextlib.nullcontext():
                     handles.append(_C.rasterize_gaussians_begin(
                         rs.bg, means3D, colors_precomp, segments, opacities, scales, rotations, rs.scale_modifier,
                         cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
@@ -298,28 +305,29 @@ class _RasterizeGaussiansMultiview(torch.autograd.Function):
         except BaseException:
             for v, h in enumerate(handles):  # every started forward is waited for (its ticket freed)
                 try:
-                    with torch.cuda.stream(side) if side is not None and (v & 1) == 1 else contextlib.nullcontext():
+                    sv = vstream(v)
+                    with torch.cuda.stream(sv) if sv is not None else contextlib.nullcontext():
                         _C.rasterize_gaussians_end(h)
                 except Exception:
                     pass
-            if side is not None:
-                main.wait_stream(side)
+            for sd in sides:
+                main.wait_stream(sd)
             raise
         for v, rs in enumerate(settings_list):
-            on_side = side is not None and (v & 1) == 1
-            with torch.cuda.stream(side) if on_side else contextlib.nullcontext():
+            sv = vstream(v)
+            with torch.cuda.stream(sv) if sv is not None else contextlib.nullcontext():
                 out = _C.rasterize_gaussians_end(handles[v])
             handles[v] = None
             num_rendered, color, depth, segment, alpha, radii, geom, binning, img = out
-            if on_side:
+            if sv is not None:
                 for t in (color, depth, segment, alpha, radii, geom, binning, img):
                     if t.is_cuda and t.numel() > 0:
                         t.record_stream(main)
             views.append((num_rendered, radii, geom, binning, img, alpha))
             ctx.mark_non_differentiable(radii)
             outs += [color, radii, depth, alpha, segment]
-        if side is not None:
-            main.wait_stream(side)
+        for sd in sides:
+            main.wait_stream(sd)
         ctx.settings_list = settings_list
         ctx.views = views
         ctx.save_for_backward(colors_precomp, segments, means3D, scales, rotations, cov3Ds_precomp, sh)
