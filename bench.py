@@ -565,7 +565,7 @@ def main():
                            f"avg_launch_ms_stage_pass; rocprofv3 --kernel-trace of this command, the same "
                            f"{n_kpass} launches picked out of the trace by tools/ktrace_phases.py "
                            f"(its kernel_stats average also holds the batched and train-step launches): "
-                           f"profiles/round5_g_kernel_phases.txt"),
+                           f"profiles/round5_t_kernel_phases.txt"),
                 "avg_launch_ms_timed_region": round(avg_window, 4) if avg_window else None,
                 "avg_launch_ms_stage_pass": round(sms[dom_i] / scnt[dom_i], 4) if scnt[dom_i] else None,
                 "valu_instr_per_launch": (pmc.get("kernels", {}).get(dom, {}).get("SQ_INSTS_VALU")
