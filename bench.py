@@ -534,8 +534,11 @@ def main():
     value = world * B * args.steps / elapsed
     roof = None
     if dom and kcnt[dom_i]:
-        avg_live = kms[dom_i] / kcnt[dom_i]  # every launch of the dedicated pass
+        avg_pass = kms[dom_i] / kcnt[dom_i]  # every launch of the dedicated pass after the timed region
         avg_window = ms[dom_i] / cnt[dom_i] if cnt[dom_i] else None  # sampled inside the timed region
+        # the line's launch time is the one measured inside the timed region (every 4th step's
+        # launch bracketed); the dedicated pass stands in only when the region had no sample
+        avg_live = avg_window if avg_window else avg_pass
         achieved = round(algorithmic_bytes(dom, P, I, HW, deg, B, written=Wrec) / (avg_live * 1e-3) / 1e9, 1)
         traffic = cyc_per_valu = None
         pmc, pmc_note = pmc_for_this_build()
@@ -557,16 +560,18 @@ def main():
                 "measured_copy_peak": measured_peak,
                 "frac_of_measured_peak": round(achieved / measured_peak, 4) if measured_peak else None,
                 "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg, B, written=Wrec),
-                "avg_launch_ms": round(avg_live, 4), "launches_timed": int(kcnt[dom_i]),
-                "timing": (f"mean of hipEvent brackets that libgsr records on its launch stream around every "
-                           f"{dom} launch of {n_kpass} steps run right after the timed region (only that stage "
-                           f"bracketed); the same bracket sampled every 4th step inside the timed region: "
-                           f"avg_launch_ms_timed_region; every stage bracketed (untimed stage pass): "
-                           f"avg_launch_ms_stage_pass; rocprofv3 --kernel-trace of this command, the same "
-                           f"{n_kpass} launches picked out of the trace by tools/ktrace_phases.py "
-                           f"(its kernel_stats average also holds the batched and train-step launches): "
+                "avg_launch_ms": round(avg_live, 4),
+                "launches_timed": int(cnt[dom_i]) if avg_window else int(kcnt[dom_i]),
+                "timing": (f"avg_launch_ms = mean of the hipEvent brackets libgsr records on its launch stream "
+                           f"around the {dom} launch of every 4th step inside the timed region (only that stage "
+                           f"bracketed there); avg_launch_ms_kernel_pass: the same bracket around every launch of "
+                           f"{n_kpass} steps run right after the timed region; avg_launch_ms_stage_pass: every stage "
+                           f"bracketed (untimed stage pass, inflated by the brackets); rocprofv3 --kernel-trace of "
+                           f"this command, the metric phase's launches picked out by tools/ktrace_phases.py (the "
+                           f"trace's kernel_stats average also holds the batched and train-step launches): "
                            f"profiles/round5_t_kernel_phases.txt"),
                 "avg_launch_ms_timed_region": round(avg_window, 4) if avg_window else None,
+                "avg_launch_ms_kernel_pass": round(avg_pass, 4),
                 "avg_launch_ms_stage_pass": round(sms[dom_i] / scnt[dom_i], 4) if scnt[dom_i] else None,
                 "valu_instr_per_launch": (pmc.get("kernels", {}).get(dom, {}).get("SQ_INSTS_VALU")
                                           if pmc is not None else None),

@@ -6,7 +6,8 @@ render_bwd then k_gaussian_backward on one stream), the streaming-copy probe, ba
 (8 render_bwd launches, then k_gaussian_backward_mv, on two overlapping streams) and the training
 step legs (a loss gradient, not the metric's upstream gradients). The profiler's kernel_stats average
 mixes all of them. This prints, for KERNEL (default k_render_bwd1), each phase's dispatch
-durations, and the metric phase's last N launches (N = --kpass, default 20) = the kernel pass.
+durations, the metric phase's last N launches (N = --kpass, default 20) = the kernel pass, and the N
+before them = the timed region (bench.py --steps N).
 
 usage: python tools/ktrace_phases.py kernel_trace.csv [KERNEL] [--kpass N]
 """
@@ -62,6 +63,8 @@ def main():
         print(f"{kern} {label:16s} {stats(v)}")
     if phases and phases[0][0] == "single" and len(phases[0][1]) >= kpass:
         print(f"{kern} metric kernel pass (last {kpass}) {stats(phases[0][1][-kpass:])}")
+        if len(phases[0][1]) >= 2 * kpass:  # the timed region's steps precede the kernel pass
+            print(f"{kern} metric timed region (the {kpass} before) {stats(phases[0][1][-2 * kpass:-kpass])}")
     if pending:
         print(f"{kern} unclassified dispatches={len(pending)}")
 
