@@ -575,7 +575,12 @@ int gsr_forward_deferred(const gsr_settings* s, const gsr_inputs* in, void* geom
                          stream);
     }
     t_slot = 0;
-    if (rc) return rc;
+    if (rc) {
+        // kernels already queued may still store into slot k's word: let them finish before the
+        // slot can be handed out again
+        (void)hipStreamSynchronize((hipStream_t)stream);
+        return rc;
+    }
     hs.busy[k] = true;
     *ticket = k;
     return 0;
@@ -607,12 +612,17 @@ int gsr_forward(const gsr_settings* s, const gsr_inputs* in, void* geom, int* ra
         // Speculative stage B: launched right behind stage A into the caller's buffer laid out
         // for C instances, the kernels reading num_rendered from device memory; the host waits
         // for num_rendered only afterwards, so no host round trip stalls the GPU.
-        if (int rc = geometry_impl(s, in, geom, radii, stream, num_rendered, false)) return rc;
+        if (int rc = geometry_impl(s, in, geom, radii, stream, num_rendered, false)) {
+            (void)hipStreamSynchronize((hipStream_t)stream);  // queued kernels may still store the slot word
+            return rc;
+        }
         const GeomLayout L = geom_layout((size_t)s->P);
         const uint32_t* n_dev = at<uint32_t>(aligned_base(geom), L.offsets) + (s->P - 1);
         if (int rc = render_impl(s, in, geom, binning, img, C, C, n_dev, out_color, out_depth, out_alpha,
-                                 out_segment, stream))
+                                 out_segment, stream)) {
+            (void)hipStreamSynchronize((hipStream_t)stream);
             return rc;
+        }
         uint32_t total = 0;
         if (int rc = wait_total(host_total_slot().host, (hipStream_t)stream, n_dev, &total)) return rc;
         if (total > 0x7FFFFFFFu) return fail("[gsr] num_rendered overflows int32");
