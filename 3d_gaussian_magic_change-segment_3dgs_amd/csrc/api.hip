@@ -385,8 +385,8 @@ int geometry_impl(const gsr_settings* s, const gsr_inputs* in, void* geom, int* 
         const bool lb = sort_uses_lookback(P) || sort_grouped_size(P);  // look-back counters to clear
         launch_preprocess(*s, *in, IL.gx, IL.gy, at<float4>(g, L.rec), radii, at<uint32_t>(g, L.tiles_touched),
                           at<uint32_t>(g, L.depth_keys), at<uint8_t>(g, L.clamped), at<ushort4>(g, L.rect),
-                          packed ? at<uint32_t>(g, L.rect32) : nullptr, at<float>(g, L.shjac), at<float>(g, L.opac),
-                          at<uint32_t>(g, L.goff), at<uint32_t>(g, L.btot), g + L.ws, lb ? sort_zero_bytes(P, depth_sort_passes()) : 0,
+                          packed ? at<uint32_t>(g, L.rect32) : nullptr, at<float>(g, L.shjac), at<float2>(g, L.og),
+                          at<uint32_t>(g, L.btot), g + L.ws, lb ? sort_zero_bytes(P, depth_sort_passes()) : 0,
                           g + L.ws_scan, scan_ws_bytes(P), st);
     }
     GSR_STAGE("preprocess");
@@ -706,9 +706,9 @@ int backward_impl(const gsr_settings* s, const gsr_inputs* in, const int* radii,
         StageScope sc(GSR_STAGE_GAUSSIAN_BWD, st);
         gsr_grads gr = *grads;
         if (sh_rows) gr.dsh = nullptr;  // deferred: the exchange writes dsh from the rows
-        launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<uint32_t>(g, GL.goff),
+        launch_gaussian_backward(*s, *in, radii, at<uint32_t>(g, GL.tiles_touched), at<float2>(g, GL.og),
                                  at<uint32_t>(g, GL.bbase),
-                                 at<uint8_t>(g, GL.clamped), contrib, written, at<float>(g, GL.opac),
+                                 at<uint8_t>(g, GL.clamped), contrib, written,
                                  at<float>(g, GL.shjac), gr, sh_rows, st);
     }
     GSR_STAGE("gaussian backward");
@@ -843,12 +843,11 @@ int backward_multiview_impl(int B, const gsr_view_state* views, const gsr_inputs
         MvView& w = a.v[v];
         w.radii = V.radii;
         w.tiles_touched = at<uint32_t>(g, GL.tiles_touched);
-        w.goff = at<uint32_t>(g, GL.goff);
         w.bbase = at<uint32_t>(g, GL.bbase);
         w.clamped = at<uint8_t>(g, GL.clamped);
         w.contrib = contrib;
         w.written = written;
-        w.opac = at<float>(g, GL.opac);
+        w.og = at<float2>(g, GL.og);
         w.shjac = at<float>(g, GL.shjac);
         w.view = s->viewmatrix;
         w.proj = s->projmatrix;
@@ -955,8 +954,7 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
     else if (n == "rec") G(GL.rec, Pz * 64);
     else if (n == "clamped") G(GL.clamped, Pz);
     else if (n == "order") G(GL.order, Pz * 4);
-    else if (n == "goff") G(GL.goff, Pz * 4);
-    else if (n == "bbase") G(GL.bbase, cdiv(Pz, (size_t)SLOT_BLOCK) * 4);
+    else if (n == "goff") G(GL.og + 4, Pz * 4);  // the odd words of the (opacity, goff) pairs
     else if (n == "bbase") G(GL.bbase, cdiv(Pz, (size_t)SLOT_BLOCK) * 4);
     else if (n == "point_list") B(BL.point_list, I * 4);
     else if (n == "slot_vals") B(BL.slot_vals, I * 4);
@@ -970,6 +968,11 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
     }
     if (!dst) return (long long)bytes;  // size query: no device access
     if (bytes == 0 || !src) return 0;   // empty, or the buffer holding it was not passed
+    if (n == "goff") {  // strided: 4 of every 8 bytes
+        if (hipMemcpy2DAsync(dst, 4, src, 8, 4, Pz, hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess)
+            return -1;
+        return (long long)bytes;
+    }
     if (hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream) != hipSuccess) return -1;
     return (long long)bytes;
 }

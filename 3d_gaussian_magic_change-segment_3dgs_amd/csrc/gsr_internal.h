@@ -131,13 +131,14 @@ size_t rows_bin_ws_bytes(size_t cap);
 
 // ---- geometry buffer (reference GeometryState, rasterizer_impl.cu:155-171) ----
 struct GeomLayout {
-    size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, goff, ws,
-        ws_scan, rect32, rect32_alt, rect32_sorted, shjac, opac, btot, bbase, bytes;
+    size_t rec, tiles_touched, depth_keys, clamped, rect, order, order_alt, dkeys_alt, offsets, ws,
+        ws_scan, rect32, rect32_alt, rect32_sorted, shjac, og, btot, bbase, bytes;
 };
 // Record slots are numbered in Gaussian-index order, per block of SLOT_BLOCK Gaussians (the
 // preprocess's blocks): Gaussian g's instance slots start at goff[g] + bbase[g / SLOT_BLOCK], where
-// goff is the exclusive scan of the tile counts inside g's block and bbase[b] the slots of the
-// blocks before b (block_bases, binning.hip, from the blocks' totals btot).
+// goff (the second word of GeomLayout::og[g]) is the exclusive scan of the tile counts inside g's
+// block and bbase[b] the slots of the blocks before b (block_bases, binning.hip, from the blocks'
+// totals btot).
 constexpr int SLOT_BLOCK = 256;
 inline GeomLayout geom_layout(size_t P) {
     GeomLayout L{};
@@ -152,7 +153,6 @@ inline GeomLayout geom_layout(size_t P) {
     L.order_alt = take(P * 4);
     L.dkeys_alt = take(P * 4);
     L.offsets = take(P * 4);
-    L.goff = take(P * 4);
     // depth sort; afterwards the row binning's level-1 table (binning_rows.hip)
     L.ws = take(std::max(sort_ws_bytes(P, MAX_SORT_PASSES), rows_bin_geom_ws_bytes(P, 255)));
     L.ws_scan = take(scan_ws_bytes(P));              // tiles_touched scan
@@ -165,9 +165,10 @@ inline GeomLayout geom_layout(size_t P) {
     // d(rgb)/d(dir) of the SH colour, 9 x 64 floats per 64 Gaussians (preprocess writes
     // it, the backward reads it instead of the 192-B SH rows; preprocess.hip sh_dir_jacobian)
     L.shjac = take(cdiv(P, 64) * 64 * 9 * 4);
-    // opacity of each visible Gaussian, for the per-Gaussian backward (which recomputes the
-    // conic and so reads no 64-B record: the record's 32-B half cost a scattered sector read)
-    L.opac = take(P * 4);
+    // (opacity, in-block first record slot) of each Gaussian, for the per-Gaussian backward (which
+    // recomputes the conic and so reads no 64-B record: the record's 32-B half cost a scattered
+    // sector read); one 8-B stream instead of two 4-B ones
+    L.og = take(P * 8);
     L.btot = take(cdiv(P, (size_t)SLOT_BLOCK) * 4);
     L.bbase = take(cdiv(P, (size_t)SLOT_BLOCK) * 4);
     L.bytes = o + ALIGN;
@@ -265,7 +266,7 @@ inline char* aligned_base(void* p) {
 // preprocess.hip
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec,
                        int* radii, uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped,
-                       ushort4* rect, uint32_t* rect32, float* shjac, float* opac, uint32_t* goff, uint32_t* btot,
+                       ushort4* rect, uint32_t* rect32, float* shjac, float2* og, uint32_t* btot,
                        void* zero_a, size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes, hipStream_t st);
 // the packed rect (GeomLayout::rect32) fits grids of up to 255 x 255 tiles (4080 px)
 inline bool rect_packable(int gx, int gy) { return gx <= 255 && gy <= 255; }
@@ -274,12 +275,11 @@ void launch_mark_visible(int P, const float* means3D, const float* view, uint8_t
 struct MvView {
     const int* radii;
     const uint32_t* tiles_touched;
-    const uint32_t* goff;
+    const float2* og;     // the view's forward GeomLayout::og (opacity, in-block first slot)
     const uint32_t* bbase;
     const uint8_t* clamped;
     const float* contrib;
     const uint8_t* written;
-    const float* opac;   // the view's forward GeomLayout::opac
     const float* shjac;  // the view's SH direction Jacobian (its forward's GeomLayout::shjac)
     const float* view;
     const float* proj;
@@ -303,8 +303,8 @@ void launch_gaussian_backward_multiview(int P, int D, int M, float scale_modifie
 void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const float* shx, float* dsh,
                         hipStream_t st);
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
-                              const uint32_t* tiles_touched, const uint32_t* goff, const uint32_t* bbase,
-                              const uint8_t* clamped, const float* contrib, const uint8_t* written, const float* opac,
+                              const uint32_t* tiles_touched, const float2* og, const uint32_t* bbase,
+                              const uint8_t* clamped, const float* contrib, const uint8_t* written,
                               const float* shjac, const gsr_grads& g, float* shx, hipStream_t st);
 // binning.hip
 // Optional last-pass outputs of a sort: ranges[key] = [first, last + 1) of each key's run in

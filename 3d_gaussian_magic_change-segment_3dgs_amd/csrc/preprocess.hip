@@ -349,7 +349,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
                                                     uint32_t* __restrict__ depth_keys,
                                                     uint8_t* __restrict__ clamped, ushort4* __restrict__ rect,
                                                     uint32_t* __restrict__ rect32, float* __restrict__ shjac,
-                                                    float* __restrict__ opac, uint32_t* __restrict__ goff,
+                                                    float2* __restrict__ og,
                                                     uint32_t* __restrict__ btot,
                                                     void* zero_a, size_t zero_a16, void* zero_b, size_t zero_b16) {
     const int idx = blockIdx.x * blockDim.x + threadIdx.x;
@@ -380,6 +380,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     }
 
     const f3 p_orig = ld3(in.means3D + 3 * (size_t)sidx);
+    const float opacity = in.opacities[sidx];
     // in_frustum (auxiliary.h:139-164)
     const f3 p_view = xform4x3(p_orig, cam.view);
     bool ok = live && p_view.z > 0.2f;
@@ -417,7 +418,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     ok = ok && ntiles != 0;
     // Record slots in Gaussian-index order: the block's exclusive scan of the tile counts here,
     // the blocks' bases from their totals btot in the depth sort's histogram kernel (bbase, see
-    // block_bases): Gaussian idx's first slot is goff[idx] + bbase[idx / 256].  Neighbouring
+    // block_bases): Gaussian idx's first slot is og[idx].y + bbase[idx / 256].  Neighbouring
     // Gaussians then own neighbouring slot ranges, which the per-Gaussian backward reads.  The wave
     // scan (DPP) runs here, the block combine after the SH work (slot_scan_finish), behind a bare
     // s_barrier: __syncthreads' fence would also wait for the SH loads in flight.
@@ -434,7 +435,7 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
         for (int w = 0; w < 4; ++w) pre += w < wave ? s_wtot[w] : 0u;
         const uint32_t slot = pre + t_incl - t_ok;
         if (threadIdx.x == 0) btot[blockIdx.x] = s_wtot[0] + s_wtot[1] + s_wtot[2] + s_wtot[3];
-        if (live) goff[idx] = slot;
+        if (live) og[idx] = make_float2(opacity, __uint_as_float(slot));  // (opacity, in-block first slot)
         return slot;
     };
 
@@ -520,7 +521,6 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
         s0 = sg.x;
         s1 = sg.y;
     }
-    const float opacity = in.opacities[idx];
     float4* R = rec + (size_t)idx * REC_F4;
     R[0] = make_float4(px, py, conic_x, conic_y);
     R[1] = make_float4(conic_z, opacity, p_view.z, s0);
@@ -533,7 +533,6 @@ __global__ void __launch_bounds__(256) k_preprocess(gsr_settings s, gsr_inputs i
     R[3] = make_float4(__uint_as_float((uint32_t)x0 | ((uint32_t)y0 << 16)),
                        __uint_as_float((uint32_t)x1 | ((uint32_t)y1 << 16)), __uint_as_float(slot0), 0.f);
     radii[idx] = (int)my_radius;
-    opac[idx] = opacity;
     tiles_touched[idx] = ntiles;
     depth_keys[idx] = __float_as_uint(p_view.z);
     clamped[idx] = cbits;
@@ -722,12 +721,11 @@ __device__ __forceinline__ void wave_gather(const float* __restrict__ contrib, c
 __global__ void __launch_bounds__(256) GSR_GBWD_ATTR k_gaussian_backward(gsr_settings s, gsr_inputs in,
                                                            const int* __restrict__ radii,
                                                            const uint32_t* __restrict__ tiles_touched,
-                                                           const uint32_t* __restrict__ goff,
+                                                           const float2* __restrict__ og,
                                                            const uint32_t* __restrict__ bbase,
                                                            const uint8_t* __restrict__ clamped,
                                                            const float* __restrict__ contrib,
                                                            const uint8_t* __restrict__ written,
-                                                           const float* __restrict__ opac,
                                                            const float* __restrict__ shjac, gsr_grads g,
                                                            float* __restrict__ shx) {
     // shx != NULL (gsr_backward_deferred_sh): the SH exchange rows of this view -- the
@@ -752,8 +750,9 @@ __global__ void __launch_bounds__(256) GSR_GBWD_ATTR k_gaussian_backward(gsr_set
     Cam cam;
     load_cam_smem(s, cam);
     const int rad = radii[ci];
-    const uint32_t lo_slot = goff[ci] + bbase[ci / SLOT_BLOCK], n_slot = tiles_touched[ci];
-    const float op = opac[ci];
+    const float2 og_i = og[ci];
+    const uint32_t lo_slot = __float_as_uint(og_i.y) + bbase[ci / SLOT_BLOCK], n_slot = tiles_touched[ci];
+    const float op = og_i.x;
     const f3 mean = ld3(in.means3D + c3i);
     float c3[6];
     float4 quat = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1082,14 +1081,15 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int D, int 
         float* drgb_v = shx && live ? shx + (size_t)v * chunk + i3 : nullptr;
         const bool vis_v = live && w.radii[ci] > 0;
         float q[12];
-        wave_gather(w.contrib, w.written, w.goff[ci] + w.bbase[ci / SLOT_BLOCK], vis_v ? w.tiles_touched[ci] : 0u, q,
-                    s_gl[threadIdx.x >> 6]);
+        const float2 og_v = w.og[ci];
+        wave_gather(w.contrib, w.written, __float_as_uint(og_v.y) + w.bbase[ci / SLOT_BLOCK],
+                    vis_v ? w.tiles_touched[ci] : 0u, q, s_gl[threadIdx.x >> 6]);
         if (!vis_v) {
             if (live && w.dmeans2D) { w.dmeans2D[i3] = 0.f; w.dmeans2D[i3 + 1] = 0.f; w.dmeans2D[i3 + 2] = 0.f; }
             if (drgb_v) { drgb_v[0] = 0.f; drgb_v[1] = 0.f; drgb_v[2] = 0.f; }
             continue;
         }
-        const float op = w.opac[idx];
+        const float op = og_v.x;
         const float dm2x = -op * q[7] * (0.5f * w.W);  // q[7] = sum q (a dx + b dy)
         const float dm2y = -op * q[8] * (0.5f * w.H);  // q[8] = sum q (b dx + c dy)
         if (w.dmeans2D) { w.dmeans2D[i3] = dm2x; w.dmeans2D[i3 + 1] = dm2y; w.dmeans2D[i3 + 2] = 0.f; }
@@ -1328,11 +1328,11 @@ __global__ void __launch_bounds__(256) k_sh_dsh(int P, int D, int M, const float
 #if GSR_PRE_PART == 1
 void launch_preprocess(const gsr_settings& s, const gsr_inputs& in, int gx, int gy, float4* rec, int* radii,
                        uint32_t* tiles_touched, uint32_t* depth_keys, uint8_t* clamped, ushort4* rect,
-                       uint32_t* rect32, float* shjac, float* opac, uint32_t* goff, uint32_t* btot, void* zero_a,
+                       uint32_t* rect32, float* shjac, float2* og, uint32_t* btot, void* zero_a,
                        size_t zero_a_bytes, void* zero_b, size_t zero_b_bytes, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_preprocess, dim3(cdiv(s.P, SLOT_BLOCK)), dim3(SLOT_BLOCK), 0, st, s, in, gx, gy, rec, radii,
-                       tiles_touched, depth_keys, clamped, rect, rect32, shjac, opac, goff, btot, zero_a,
+                       tiles_touched, depth_keys, clamped, rect, rect32, shjac, og, btot, zero_a,
                        cdiv(zero_a_bytes, 16), zero_b, cdiv(zero_b_bytes, 16));
 }
 
@@ -1365,12 +1365,12 @@ void launch_sh_backward(int P, int D, int M, const float* means3D, int V, const 
 
 #if GSR_PRE_PART == 2
 void launch_gaussian_backward(const gsr_settings& s, const gsr_inputs& in, const int* radii,
-                              const uint32_t* tiles_touched, const uint32_t* goff, const uint32_t* bbase,
-                              const uint8_t* clamped, const float* contrib, const uint8_t* written, const float* opac,
+                              const uint32_t* tiles_touched, const float2* og, const uint32_t* bbase,
+                              const uint8_t* clamped, const float* contrib, const uint8_t* written,
                               const float* shjac, const gsr_grads& g, float* shx, hipStream_t st) {
     if (s.P == 0) return;
     hipLaunchKernelGGL(k_gaussian_backward, dim3(cdiv(s.P, 256)), dim3(256), 0, st, s, in, radii, tiles_touched,
-                       goff, bbase, clamped, contrib, written, opac, shjac, g, in.shs ? shx : nullptr);
+                       og, bbase, clamped, contrib, written, shjac, g, in.shs ? shx : nullptr);
 }
 
 #endif  // GSR_PRE_PART == 2
