@@ -283,3 +283,13 @@ def test_multiview_deferred_forward_rebinning(gpu_available):
         for a, b in zip(o, r):
             assert torch.equal(a, b)
     assert max(_C._last_rendered[dev]) > 4097  # the counts were above the guess
+
+
+@pytest.mark.parametrize("streams", [3, 4])
+def test_multiview_forward_streams(gpu_available, streams, monkeypatch):
+    """Views dealt over more forward streams (GSR_MV_FWD_STREAMS): the same outputs and gradients."""
+    import diff_gaussian_rasterization as dgr
+    monkeypatch.setattr(dgr, "_MV_FWD_STREAMS", streams)
+    scene = synthetic_scene(4000, sh_degree=3, seed=48)
+    d = _leaves(scene)
+    _check(d, _views(5, 3))
