@@ -1076,14 +1076,31 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int D, int 
     f3 dmean_sum = {0.f, 0.f, 0.f}, dcol = {0.f, 0.f, 0.f};
     float dcv_sum[6] = {0, 0, 0, 0, 0, 0};
     float dop = 0.f, dseg0 = 0.f, dseg1 = 0.f;
+    // the next view's per-Gaussian inputs are loaded while this view's records are gathered (one
+    // round trip less in each view's chain of loads -> flags -> records)
+    struct MvIn {
+        int rad;
+        uint32_t tt;
+        float2 og;
+        uint32_t cb;
+    };
+    auto load_in = [&](int v) {
+        const MvView& w = a.v[v];
+        return MvIn{w.radii[ci], w.tiles_touched[ci], w.og[ci], in.shs ? (uint32_t)w.clamped[ci] : 0u};
+    };
+    MvIn cur = load_in(0);
     for (int v = 0; v < a.B; ++v) {  // uniform: the view's fields are scalar loads
         const MvView& w = a.v[v];
+        const MvIn nxt = v + 1 < a.B ? load_in(v + 1) : cur;
         float* drgb_v = shx && live ? shx + (size_t)v * chunk + i3 : nullptr;
-        const bool vis_v = live && w.radii[ci] > 0;
+        const bool vis_v = live && cur.rad > 0;
         float q[12];
-        const float2 og_v = w.og[ci];
-        wave_gather(w.contrib, w.written, __float_as_uint(og_v.y) + w.bbase[ci / SLOT_BLOCK],
-                    vis_v ? w.tiles_touched[ci] : 0u, q, s_gl[threadIdx.x >> 6]);
+        const float2 og_v = cur.og;
+        const uint32_t cbits_v = cur.cb;
+        const uint32_t tt_v = cur.tt;
+        cur = nxt;
+        wave_gather(w.contrib, w.written, __float_as_uint(og_v.y) + w.bbase[ci / SLOT_BLOCK], vis_v ? tt_v : 0u, q,
+                    s_gl[threadIdx.x >> 6]);
         if (!vis_v) {
             if (live && w.dmeans2D) { w.dmeans2D[i3] = 0.f; w.dmeans2D[i3 + 1] = 0.f; w.dmeans2D[i3 + 2] = 0.f; }
             if (drgb_v) { drgb_v[0] = 0.f; drgb_v[1] = 0.f; drgb_v[2] = 0.f; }
@@ -1099,7 +1116,7 @@ __global__ void __launch_bounds__(256) k_gaussian_backward_mv(int P, int D, int 
         dseg1 += q[4];
         f3 dRGB = {0.f, 0.f, 0.f};  // the clamped colour gradient (backward.cu:72-74)
         if (in.shs) {
-            const uint8_t cbits = w.clamped[idx];
+            const uint32_t cbits = cbits_v;
             dRGB = {(cbits & 1) ? 0.f : q[0], (cbits & 2) ? 0.f : q[1], (cbits & 4) ? 0.f : q[2]};
         }
         if (drgb_v) {
