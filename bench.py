@@ -195,15 +195,19 @@ def cpu_baseline(scene, cam, grads, budget_s=20.0):
     r1 = 20
     tf1, tb1 = views(s1, c1, up1, r1)
     O.lib().oracle_set_num_threads(share)
-    return {"value": allc["value"], "unit": "views/s", "cores": allc["threads"],
-            "cores_note": (f"OpenMP threads = every CPU sched_getaffinity allows ({affinity} of the machine's "
-                           f"os.cpu_count()={os.cpu_count()} logical CPUs, shared with other GPUs' jobs); "
-                           f"'pool_share' = the same timed on OMP_NUM_THREADS={os.environ.get('OMP_NUM_THREADS')} "
-                           f"threads, the pool's CPU share for one GPU"),
+    # the machine's CPUs are shared with other GPUs' jobs, so every CPU is not always the faster
+    # setting: `value` is the faster of the two thread counts (the baseline is not handicapped)
+    best = pool if pool and pool["value"] > allc["value"] else allc
+    return {"value": best["value"], "unit": "views/s", "cores": best["threads"],
+            "cores_note": (f"`value` = the faster of two timings: OpenMP threads = every CPU sched_getaffinity "
+                           f"allows ({affinity} of the machine's os.cpu_count()={os.cpu_count()} logical CPUs, "
+                           f"shared with other GPUs' jobs: 'all_cpus') and OMP_NUM_THREADS="
+                           f"{os.environ.get('OMP_NUM_THREADS')} threads, the pool's CPU share for one GPU "
+                           f"('pool_share')"),
             "affinity_cpus": affinity, "machine_cpus": os.cpu_count(),
             "kind": "port", "cpu_model": cpu_model(),
-            "fwd_ms_per_view": allc["fwd_ms_per_view"], "bwd_ms_per_view": allc["bwd_ms_per_view"],
-            "pool_share": pool,
+            "fwd_ms_per_view": best["fwd_ms_per_view"], "bwd_ms_per_view": best["bwd_ms_per_view"],
+            "all_cpus": allc, "pool_share": pool,
             "c1": {"value": round(r1 / (tf1 + tb1), 2), "unit": "views/s", "fwd_ms_per_view": round(1e3 * tf1 / r1, 2),
                    "bwd_ms_per_view": round(1e3 * tb1 / r1, 2), "threads": affinity or share,
                    "sample": f"{r1} views of C1 (P={s1.P}, {c1.width}x{c1.height}, SH{s1.sh_degree})"},
