@@ -228,7 +228,7 @@ def test_zero_gaussians(gpu_available):
                                  segments=torch.zeros(0, 2, device="cuda"), scales=torch.zeros(0, 3, device="cuda"),
                                  rotations=torch.zeros(0, 4, device="cuda"))
     color, radii, depth, alpha, segment = out
-    assert color.shape == (3, 32, 48) and float(color.abs().sum()) == 0.0 and radii.numel() == 0
+    assert color.shape == (3, 32, 48) and color.detach().abs().sum().item() == 0.0 and radii.numel() == 0
 
 
 def test_table_mode_sorts(gpu_available, oracle_mod):
