@@ -592,12 +592,16 @@ int gsr_forward_wait(int ticket, const gsr_settings* s, const void* geom, void* 
     if (ticket < 1 || ticket >= HOST_SLOTS) return fail("[gsr] forward_wait: not a pending ticket");
     HostSlots& hs = host_slots();
     if (!hs.busy[ticket]) return fail("[gsr] forward_wait: not a pending ticket");
-    hs.busy[ticket] = false;
+    // a bad call keeps the ticket pending: its kernels may still store into the slot's word,
+    // so the slot must not be handed to the next gsr_forward_deferred
     if (!s || !geom || !num_rendered || s->P <= 0) return fail("[gsr] forward_wait: null argument");
     const GeomLayout L = geom_layout((size_t)s->P);
     const uint32_t* n_dev = at<uint32_t>(aligned_base(const_cast<void*>(geom)), L.offsets) + (s->P - 1);
     uint32_t total = 0;
-    if (int rc = wait_total(hs.host ? hs.host + 16 * ticket : nullptr, (hipStream_t)stream, n_dev, &total)) return rc;
+    const int rc = wait_total(hs.host ? hs.host + 16 * ticket : nullptr, (hipStream_t)stream, n_dev, &total);
+    if (rc) (void)hipStreamSynchronize((hipStream_t)stream);  // nothing may store the word after release
+    hs.busy[ticket] = false;
+    if (rc) return rc;
     if (total > 0x7FFFFFFFu) return fail("[gsr] num_rendered overflows int32");
     *num_rendered = (int)total;
     return total > (uint32_t)s->binning_capacity ? GSR_NEED_BINNING : 0;
@@ -957,7 +961,15 @@ long long gsr_debug_copy(const char* name, int P, int W, int H, int num_rendered
     else if (n == "goff") G(GL.og + 4, Pz * 4);  // the odd words of the (opacity, goff) pairs
     else if (n == "bbase") G(GL.bbase, cdiv(Pz, (size_t)SLOT_BLOCK) * 4);
     else if (n == "point_list") B(BL.point_list, I * 4);
-    else if (n == "slot_vals") B(BL.slot_vals, I * 4);
+    else if (n == "slot_vals") {
+        // only the radix binning (grids beyond 255 x 255 tiles, or row binning switched off)
+        // writes it; the row binning derives record slots from the record
+        if (g_rows_binning && rect_packable(IL.gx, IL.gy)) {
+            fail("[gsr] debug_copy: slot_vals is not materialised by the row binning");
+            return -1;
+        }
+        B(BL.slot_vals, I * 4);
+    }
     else if (n == "written") B(BL.written, I);  // the backward's written-record flags (1 byte per slot)
     else if (n == "ranges") M(IL.ranges, T * 8);
     else if (n == "n_contrib_tiles") M(IL.n_contrib, T * TILE_PIX * 4);

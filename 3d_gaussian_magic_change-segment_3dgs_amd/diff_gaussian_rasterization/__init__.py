@@ -302,32 +302,35 @@ class _RasterizeGaussiansMultiview(torch.autograd.Function):
                         rs.bg, means3D, colors_precomp, segments, opacities, scales, rotations, rs.scale_modifier,
                         cov3Ds_precomp, rs.viewmatrix, rs.projmatrix, rs.tanfovx, rs.tanfovy, rs.image_height,
                         rs.image_width, sh, rs.sh_degree, rs.campos, rs.prefiltered, rs.debug))
+            for v, rs in enumerate(settings_list):
+                sv = vstream(v)
+                h, handles[v] = handles[v], None   # ended (its ticket freed) even if _end raises
+                with torch.cuda.stream(sv) if sv is not None else contextlib.nullcontext():
+                    out = _C.rasterize_gaussians_end(h)
+                num_rendered, color, depth, segment, alpha, radii, geom, binning, img = out
+                if sv is not None:
+                    for t in (color, depth, segment, alpha, radii, geom, binning, img):
+                        if t.is_cuda and t.numel() > 0:
+                            t.record_stream(main)
+                views.append((num_rendered, radii, geom, binning, img, alpha))
+                ctx.mark_non_differentiable(radii)
+                outs += [color, radii, depth, alpha, segment]
         except BaseException:
-            for v, h in enumerate(handles):  # every started forward is waited for (its ticket freed)
+            # every started forward that has not been ended is ended now (tickets are per-thread
+            # pinned slots, GSR_MAX_DEFERRED of them: a leaked one fails every later batch)
+            for v, h in enumerate(handles):
+                if h is None:
+                    continue
                 try:
                     sv = vstream(v)
                     with torch.cuda.stream(sv) if sv is not None else contextlib.nullcontext():
                         _C.rasterize_gaussians_end(h)
                 except Exception:
                     pass
+            raise
+        finally:
             for sd in sides:
                 main.wait_stream(sd)
-            raise
-        for v, rs in enumerate(settings_list):
-            sv = vstream(v)
-            with torch.cuda.stream(sv) if sv is not None else contextlib.nullcontext():
-                out = _C.rasterize_gaussians_end(handles[v])
-            handles[v] = None
-            num_rendered, color, depth, segment, alpha, radii, geom, binning, img = out
-            if sv is not None:
-                for t in (color, depth, segment, alpha, radii, geom, binning, img):
-                    if t.is_cuda and t.numel() > 0:
-                        t.record_stream(main)
-            views.append((num_rendered, radii, geom, binning, img, alpha))
-            ctx.mark_non_differentiable(radii)
-            outs += [color, radii, depth, alpha, segment]
-        for sd in sides:
-            main.wait_stream(sd)
         ctx.settings_list = settings_list
         ctx.views = views
         ctx.save_for_backward(colors_precomp, segments, means3D, scales, rotations, cov3Ds_precomp, sh)

@@ -11,8 +11,13 @@ The parent never touches the GPU (no HIP call, no torch.cuda query that initiali
 the runtime): it only spawns, waits and relays.  The ranks are child processes, not an
 exec of the parent.  If one rank exits non-zero the others are given a grace period
 (they are usually blocked in a collective with the dead rank) and then terminated by
-their exact PIDs; the parent exits with the first failing rank's status.
+their exact PIDs; the parent exits with the first failing rank's status.  A rank that
+outlives a rank that finished normally by more than the straggler grace period (stuck in a
+collective the finished rank never joins) is terminated too, and the job exits 124: a hang
+ends the job instead of running into the driver's time limit.  Collectives themselves time
+out after dist_timeout() seconds (bench.py passes it to init_process_group).
 """
+import datetime
 import os
 import signal
 import socket
@@ -23,6 +28,17 @@ import time
 
 RANK_ENV = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT",
             "GROUP_RANK", "ROLE_RANK", "ROLE_WORLD_SIZE")
+
+
+STRAGGLER_STATUS = 124
+
+
+def dist_timeout(env=None):
+    """The process group's timeout (rendezvous and every collective): GSR_DIST_TIMEOUT_S,
+    default 300 s -- long enough for a fresh box's first import of torch on every rank, short
+    against the driver's limit."""
+    env = os.environ if env is None else env
+    return datetime.timedelta(seconds=float(env.get("GSR_DIST_TIMEOUT_S", "300")))
 
 
 def free_port(host="127.0.0.1"):
@@ -49,11 +65,12 @@ def _pump(src, dst):
     src.close()
 
 
-def spawn_ranks(world, argv, grace_s=30.0, poll_s=0.05, port=None, env=None):
+def spawn_ranks(world, argv, grace_s=30.0, poll_s=0.05, port=None, env=None, straggler_s=60.0):
     """Run `argv` (a full command line: [python, script, args...]) as `world` ranks of one
     node.  Rank 0's stdout becomes this process's stdout, every other rank's stdout goes to
     stderr; stderr is inherited.  Returns the job's exit status: 0 if every rank exited 0,
-    else the first non-zero status seen (a rank killed by a signal reports 128 + signal)."""
+    else the first non-zero status seen (a rank killed by a signal reports 128 + signal), or
+    STRAGGLER_STATUS when ranks had to be terminated straggler_s after a rank exited 0."""
     if world < 1:
         raise ValueError("world must be >= 1")
     base = dict(os.environ if env is None else env)
@@ -71,6 +88,7 @@ def spawn_ranks(world, argv, grace_s=30.0, poll_s=0.05, port=None, env=None):
             pumps.append(t)
         status = 0
         failed_at = None
+        first_ok = None  # (time, rank) of the first rank that exited 0
         alive = set(range(world))
         while alive:
             for r in sorted(alive):
@@ -83,7 +101,15 @@ def spawn_ranks(world, argv, grace_s=30.0, poll_s=0.05, port=None, env=None):
                     failed_at = time.monotonic()
                     print(f"[launch] rank {r} exited with status {rc}; waiting {grace_s:g} s for the others",
                           file=sys.stderr, flush=True)
-            if alive and failed_at is not None and time.monotonic() - failed_at > grace_s:
+                elif rc == 0 and first_ok is None:
+                    first_ok = (time.monotonic(), r)
+            now = time.monotonic()
+            stuck = alive and failed_at is None and first_ok is not None and now - first_ok[0] > straggler_s
+            if stuck:
+                print(f"[launch] rank(s) {sorted(alive)} still running {straggler_s:g} s after rank {first_ok[1]} "
+                      f"exited 0 (a collective nobody else joins?)", file=sys.stderr, flush=True)
+                status = STRAGGLER_STATUS
+            if alive and (stuck or (failed_at is not None and now - failed_at > grace_s)):
                 for r in sorted(alive):
                     print(f"[launch] terminating rank {r} (pid {procs[r].pid})", file=sys.stderr, flush=True)
                     _stop(procs[r])

@@ -286,11 +286,14 @@ def main():
     # so a one-GPU box runs the exchange through RCCL exactly as the N-GPU bench issues it
     if world > 1 or os.environ.get("GSR_DIST_FORCE") == "1":
         import torch.distributed as dist
+        from gsr_tools.launch import dist_timeout
         backend = os.environ.get("GSR_DIST_BACKEND", "nccl")  # nccl == RCCL over xGMI on ROCm
+        # a bounded timeout (rendezvous and every collective; RCCL's watchdog aborts a stuck
+        # collective after it): a hung rank fails the job instead of burning the driver's limit
         if backend == "nccl":
-            dist.init_process_group(backend, device_id=device)
+            dist.init_process_group(backend, device_id=device, timeout=dist_timeout())
         else:
-            dist.init_process_group(backend)
+            dist.init_process_group(backend, timeout=dist_timeout())
     native_dp = False
 
     from gsr_tools.scene import config_scene_and_camera

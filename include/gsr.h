@@ -294,7 +294,9 @@ GSR_API int gsr_mark_visible(int P, const float* means3D, const float* viewmatri
  * seg0,r,g,b,seg1,0...}), "clamped" u8[P], "order" u32[P] (depth order),
  * "goff" u32[P] (the Gaussian's first record slot inside its block of 256 Gaussians: slots are
  * numbered in Gaussian-index order), "bbase" u32[ceil(P/256)] (the slots before each block),
- * "point_list" u32[I], "slot_vals" u32[I], "ranges" u32[T,2],
+ * "point_list" u32[I], "slot_vals" u32[I] (the radix binning's instance slots: -1 with an
+ * error when the row binning -- the default for grids up to 255 x 255 tiles -- is active, as it
+ * writes none), "ranges" u32[T,2],
  * "n_contrib_tiles" u32[T,256] (tile-major, in the forward's 8x8-quadrant layout:
  * entry k*64+l of tile (tx, ty) is pixel (16*tx + 8*(k&1) + (l&7), 16*ty + 8*(k>>1) + (l>>3)),
  * k = 0..3 the quadrant, l = 0..63 the lane), "written" u8[I] (after a backward: 1 at

@@ -63,6 +63,41 @@ static inline v3 operator*(v3 a, float s) { return {a.x * s, a.y * s, a.z * s}; 
 static inline v3 operator/(v3 a, float s) { return {a.x / s, a.y / s, a.z / s}; }
 static inline float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 
+// ---------------------------------------------------------------------------------------------
+// nvcc contraction model (VERDICT r5 "Next" #1).  DGR is built with nvcc's defaults
+// (DGR/setup.py:17-34: --fmad=true, no fast-math), so the reference binary contracts a*b+c into
+// FMAs, while this oracle (-ffp-contract=off) and gsr round twice.  With g_contract != 0 the
+// oracle evaluates the sites that decide integer outputs the way LLVM's DAG combiner (NVVM's
+// code generator) contracts them:
+//   * fadd/fsub of a bare product and anything: the product is fused (fma(a, b, +-z));
+//   * of two bare products: the LEFT one is fused, the right one rounded (equal use counts;
+//     CT_RIGHT fuses the right one instead, to bracket the model);
+//   * a sum chain p0 + p1 + p2 (+ c): fma(a2, b2, fma(a0, b0, p1)) (+ c) -- the running sum
+//     is no longer a bare product, so each later product is fused into it.
+// Bits: CT_PRE = projection (auxiliary.h:58-77 transformPoint4x3/4x4, in_frustum :139-164),
+// ndc2Pix (:41-44, in double), computeCov3D (forward.cu:118-152), computeCov2D (:74-113), the
+// determinant / eigenvalue / radius lines (:219-232); CT_BLEND = the blend's power and its
+// colour / weight / depth / segment sums (forward.cu:346, 362-366; the backward's power,
+// backward.cu:541, so the replay sees the forward's decisions).  Default 0 = gsr's evaluation.
+// ptxas may fuse further pairs on its own; the model does not claim to be the binary, it
+// measures how many integer outputs a last-bit change of this kind moves.
+enum { CT_PRE = 1, CT_BLEND = 2, CT_RIGHT = 4 };
+static int g_contract = 0;
+static inline float pp_add(int c, float a, float b, float x, float y) {  // a*b + x*y
+    if (!c) return a * b + x * y;
+    return (c & CT_RIGHT) ? std::fma(x, y, a * b) : std::fma(a, b, x * y);
+}
+static inline float pp_sub(int c, float a, float b, float x, float y) {  // a*b - x*y
+    if (!c) return a * b - x * y;
+    return (c & CT_RIGHT) ? std::fma(-x, y, a * b) : std::fma(a, b, -(x * y));
+}
+static inline float dot3c(int c, float a0, float b0, float a1, float b1, float a2, float b2) {
+    if (!c) return a0 * b0 + a1 * b1 + a2 * b2;
+    return std::fma(a2, b2, pp_add(c, a0, b0, a1, b1));
+}
+static inline int ct_pre() { return (g_contract & CT_PRE) ? (g_contract | CT_PRE) : 0; }
+static inline int ct_blend() { return (g_contract & CT_BLEND) ? (g_contract | CT_BLEND) : 0; }
+
 // glm mat3: m[col][row]; mat3(a..i) fills columns.
 struct m3 { float m[3][3]; };
 static inline m3 mk(float a, float b, float c, float d, float e, float f, float g, float h, float i) {
@@ -72,11 +107,11 @@ static inline m3 mk(float a, float b, float c, float d, float e, float f, float 
     r.m[2][0] = g; r.m[2][1] = h; r.m[2][2] = i;
     return r;
 }
-static inline m3 mul(const m3& A, const m3& B) {
+static inline m3 mul(const m3& A, const m3& B, int ct = 0) {
     m3 R;
     for (int c = 0; c < 3; ++c)
         for (int r = 0; r < 3; ++r)
-            R.m[c][r] = A.m[0][r] * B.m[c][0] + A.m[1][r] * B.m[c][1] + A.m[2][r] * B.m[c][2];
+            R.m[c][r] = dot3c(ct, A.m[0][r], B.m[c][0], A.m[1][r], B.m[c][1], A.m[2][r], B.m[c][2]);
     return R;
 }
 static inline m3 tr(const m3& A) {
@@ -94,7 +129,10 @@ static inline m3 smul(float s, const m3& A) {
 static inline v3 col(const m3& A, int c) { return {A.m[c][0], A.m[c][1], A.m[c][2]}; }
 
 // auxiliary.h:41-44 (double arithmetic, float result)
-static inline float ndc2Pix(float v, int S) { return (float)(((v + 1.0) * S - 1.0) * 0.5); }
+static inline float ndc2Pix(float v, int S, int ct = 0) {
+    if (ct) return (float)(std::fma((double)v + 1.0, (double)S, -1.0) * 0.5);
+    return (float)(((v + 1.0) * S - 1.0) * 0.5);
+}
 
 // auxiliary.h:46-56
 static inline void getRect(float px, float py, int max_radius, int gx, int gy,
@@ -106,17 +144,17 @@ static inline void getRect(float px, float py, int max_radius, int gx, int gy,
 }
 
 // auxiliary.h:58-77
-static inline v3 xform4x3(v3 p, const float* m) {
-    return {m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
-            m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
-            m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14]};
+static inline v3 xform4x3(v3 p, const float* m, int ct = 0) {
+    return {dot3c(ct, m[0], p.x, m[4], p.y, m[8], p.z) + m[12],
+            dot3c(ct, m[1], p.x, m[5], p.y, m[9], p.z) + m[13],
+            dot3c(ct, m[2], p.x, m[6], p.y, m[10], p.z) + m[14]};
 }
 struct v4 { float x, y, z, w; };
-static inline v4 xform4x4(v3 p, const float* m) {
-    return {m[0] * p.x + m[4] * p.y + m[8] * p.z + m[12],
-            m[1] * p.x + m[5] * p.y + m[9] * p.z + m[13],
-            m[2] * p.x + m[6] * p.y + m[10] * p.z + m[14],
-            m[3] * p.x + m[7] * p.y + m[11] * p.z + m[15]};
+static inline v4 xform4x4(v3 p, const float* m, int ct = 0) {
+    return {dot3c(ct, m[0], p.x, m[4], p.y, m[8], p.z) + m[12],
+            dot3c(ct, m[1], p.x, m[5], p.y, m[9], p.z) + m[13],
+            dot3c(ct, m[2], p.x, m[6], p.y, m[10], p.z) + m[14],
+            dot3c(ct, m[3], p.x, m[7], p.y, m[11], p.z) + m[15]};
 }
 // auxiliary.h:89-97
 static inline v3 xformVecT(v3 p, const float* m) {
@@ -220,32 +258,40 @@ static v3 colorFromSH(int idx, int deg, int max_coeffs, const float* means, v3 c
 
 // forward.cu:74-113
 static void cov2D(v3 mean, float fx, float fy, float tanx, float tany, const float* c3,
-                  const float* view, float out[3]) {
-    v3 t = xform4x3(mean, view);
+                  const float* view, float out[3], int ct = 0) {
+    v3 t = xform4x3(mean, view, ct);
     const float limx = 1.3f * tanx, limy = 1.3f * tany;
     const float txtz = t.x / t.z, tytz = t.y / t.z;
     t.x = std::min(limx, std::max(-limx, txtz)) * t.z;
     t.y = std::min(limy, std::max(-limy, tytz)) * t.z;
     m3 J = mk(fx / t.z, 0.0f, -(fx * t.x) / (t.z * t.z), 0.0f, fy / t.z, -(fy * t.y) / (t.z * t.z), 0, 0, 0);
     m3 W = mk(view[0], view[4], view[8], view[1], view[5], view[9], view[2], view[6], view[10]);
-    m3 T = mul(W, J);
+    m3 T = mul(W, J, ct);
     m3 Vrk = mk(c3[0], c3[1], c3[2], c3[1], c3[3], c3[4], c3[2], c3[4], c3[5]);
-    m3 cov = mul(mul(tr(T), tr(Vrk)), T);
+    m3 cov = mul(mul(tr(T), tr(Vrk), ct), T, ct);
     cov.m[0][0] += 0.3f;
     cov.m[1][1] += 0.3f;
     out[0] = cov.m[0][0]; out[1] = cov.m[0][1]; out[2] = cov.m[1][1];
 }
 
 // forward.cu:118-152
-static void cov3D(v3 scale, float mod, const float* rot, float* out) {
+static void cov3D(v3 scale, float mod, const float* rot, float* out, int ct = 0) {
     m3 S = mk(1, 0, 0, 0, 1, 0, 0, 0, 1);
     S.m[0][0] = mod * scale.x; S.m[1][1] = mod * scale.y; S.m[2][2] = mod * scale.z;
     float r = rot[0], x = rot[1], y = rot[2], z = rot[3];
-    m3 R = mk(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
-              2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
-              2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
-    m3 M = mul(S, R);
-    m3 Sig = mul(tr(M), M);
+    m3 R;
+    if (!ct) {
+        R = mk(1.f - 2.f * (y * y + z * z), 2.f * (x * y - r * z), 2.f * (x * z + r * y),
+               2.f * (x * y + r * z), 1.f - 2.f * (x * x + z * z), 2.f * (y * z - r * x),
+               2.f * (x * z - r * y), 2.f * (y * z + r * x), 1.f - 2.f * (x * x + y * y));
+    } else {  // 1 - 2*s: fsub(1, fmul(2, s)) -> fma(-2, s, 1)
+        auto one_m2 = [&](float a, float b) { return std::fma(-2.f, pp_add(ct, a, a, b, b), 1.f); };
+        R = mk(one_m2(y, z), 2.f * pp_sub(ct, x, y, r, z), 2.f * pp_add(ct, x, z, r, y),
+               2.f * pp_add(ct, x, y, r, z), one_m2(x, z), 2.f * pp_sub(ct, y, z, r, x),
+               2.f * pp_sub(ct, x, z, r, y), 2.f * pp_add(ct, y, z, r, x), one_m2(x, y));
+    }
+    m3 M = mul(S, R, ct);
+    m3 Sig = mul(tr(M), M, ct);
     out[0] = Sig.m[0][0]; out[1] = Sig.m[0][1]; out[2] = Sig.m[0][2];
     out[3] = Sig.m[1][1]; out[4] = Sig.m[1][2]; out[5] = Sig.m[2][2];
 }
@@ -294,11 +340,20 @@ static inline float gsr_expf(float x) {
     return p * scale;
 }
 static inline float oracle_exp(float x) { return g_exp_libm ? std::exp(x) : gsr_expf(x); }
-// g_exp_jitter != 0: every blend exp (forward and backward alike) moves by -1 .. +1 ulp, chosen
-// by a hash of (seed, Gaussian, pixel) -- the reference algorithm run with a different faithful
-// exp, to measure each output element's own sensitivity to last-bit alpha differences
-// (tests/test_gpu_exp_budget.py).
+// forward.cu:346 / backward.cu:541: -0.5*(cx*dx*dx + cz*dy*dy) - cy*dx*dy; cb != 0: as nvcc
+// contracts it (see the contraction model above)
+static inline float blend_power(int cb, const float* co, float dx, float dy) {
+    if (!cb) return -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+    const float q = pp_add(cb, co[0] * dx, dx, co[2] * dy, dy);
+    return (cb & CT_RIGHT) ? std::fma(-(co[1] * dx), dy, -0.5f * q) : std::fma(-0.5f, q, -((co[1] * dx) * dy));
+}
+// g_exp_jitter != 0: every blend exp (forward and backward alike) moves by -n .. +n ulp
+// (n = g_exp_jitter_ulps, default 1), chosen by a hash of (seed, Gaussian, pixel) -- the
+// reference algorithm run with another exp of n-ulp accuracy around gsr_expf (CUDA's expf is
+// specified at 2 ulp), to measure each output element's own sensitivity to last-bit alpha
+// differences (tests/test_gpu_exp_budget.py).
 static uint32_t g_exp_jitter = 0;
+static int g_exp_jitter_ulps = 1;
 static inline float jitter_exp(float G, uint32_t g, uint32_t pix) {
     if (!g_exp_jitter || !(G > 0.f)) return G;
     uint64_t h = ((uint64_t)g_exp_jitter << 40) ^ ((uint64_t)g << 20) ^ (uint64_t)pix;
@@ -307,8 +362,8 @@ static inline float jitter_exp(float G, uint32_t g, uint32_t pix) {
     h ^= h >> 33;
     h *= 0xc4ceb9fe1a85ec53ull;
     h ^= h >> 33;
-    // -1 .. +1 ulp
-    int r = (int)(h % 3u) - 1;
+    // -n .. +n ulp
+    int r = (int)(h % (uint64_t)(2 * g_exp_jitter_ulps + 1)) - g_exp_jitter_ulps;
     for (; r < 0; ++r) G = std::nextafter(G, 0.0f);
     for (; r > 0; --r) G = std::nextafter(G, 2.0f * G);
     return G;
@@ -325,6 +380,9 @@ const char* oracle_last_error(void) { return g_err.c_str(); }
 void oracle_set_acc32(int on) { g_acc32 = on; }
 void oracle_set_exp_libm(int on) { g_exp_libm = on; }
 void oracle_set_exp_jitter(unsigned seed) { g_exp_jitter = seed; }
+void oracle_set_exp_jitter_ulps(int n) { g_exp_jitter_ulps = n < 1 ? 1 : n; }
+void oracle_set_contract(int mode) { g_contract = mode; }
+int oracle_get_contract(void) { return g_contract; }
 float oracle_expf(float x) { return gsr_expf(x); }
 
 int oracle_num_threads(void) {
@@ -368,13 +426,14 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
     const v3 campos = {s.campos[0], s.campos[1], s.campos[2]};
 
     // preprocessCUDA (forward.cu:154-256)
+    const int ct = ct_pre();
 #pragma omp parallel for schedule(static)
     for (int idx = 0; idx < P; ++idx) {
         v3 p_orig = {in->means3D[3 * idx], in->means3D[3 * idx + 1], in->means3D[3 * idx + 2]};
         // in_frustum (auxiliary.h:139-164)
-        v3 p_view = xform4x3(p_orig, s.view);
+        v3 p_view = xform4x3(p_orig, s.view, ct);
         if (p_view.z <= 0.2f) continue;  // prefiltered trap is a device abort; not modelled
-        v4 p_hom = xform4x4(p_orig, s.proj);
+        v4 p_hom = xform4x4(p_orig, s.proj, ct);
         float p_w = 1.0f / (p_hom.w + 0.0000001f);
         v3 p_proj = {p_hom.x * p_w, p_hom.y * p_w, p_hom.z * p_w};
         const float* c3;
@@ -382,20 +441,21 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
             c3 = in->cov3D_precomp + 6 * (size_t)idx;
         } else {
             v3 sc = {in->scales[3 * idx], in->scales[3 * idx + 1], in->scales[3 * idx + 2]};
-            cov3D(sc, s.scale_modifier, in->rotations + 4 * (size_t)idx, &st->cov3D[6 * (size_t)idx]);
+            cov3D(sc, s.scale_modifier, in->rotations + 4 * (size_t)idx, &st->cov3D[6 * (size_t)idx], ct);
             c3 = &st->cov3D[6 * (size_t)idx];
         }
         float cov[3];
-        cov2D(p_orig, focal_x, focal_y, s.tanfovx, s.tanfovy, c3, s.view, cov);
-        float det = (cov[0] * cov[2] - cov[1] * cov[1]);
+        cov2D(p_orig, focal_x, focal_y, s.tanfovx, s.tanfovy, c3, s.view, cov, ct);
+        float det = pp_sub(ct, cov[0], cov[2], cov[1], cov[1]);
         if (det == 0.0f) continue;
         float det_inv = 1.f / det;
         float conic[3] = {cov[2] * det_inv, -cov[1] * det_inv, cov[0] * det_inv};
         float mid = 0.5f * (cov[0] + cov[2]);
-        float lambda1 = mid + std::sqrt(std::max(0.1f, mid * mid - det));
-        float lambda2 = mid - std::sqrt(std::max(0.1f, mid * mid - det));
+        const float disc = ct ? std::fma(mid, mid, -det) : mid * mid - det;
+        float lambda1 = mid + std::sqrt(std::max(0.1f, disc));
+        float lambda2 = mid - std::sqrt(std::max(0.1f, disc));
         float my_radius = std::ceil(3.f * std::sqrt(std::max(lambda1, lambda2)));
-        float pix_x = ndc2Pix(p_proj.x, W), pix_y = ndc2Pix(p_proj.y, H);
+        float pix_x = ndc2Pix(p_proj.x, W, ct), pix_y = ndc2Pix(p_proj.y, H, ct);
         int minx, miny, maxx, maxy;
         getRect(pix_x, pix_y, (int)my_radius, gx, gy, minx, miny, maxx, maxy);
         if ((uint32_t)((maxx - minx) * (maxy - miny)) == 0) continue;
@@ -479,6 +539,7 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
     st->alpha.assign((size_t)W * H, 0.f);
     const float* feat = in->colors_precomp ? in->colors_precomp : st->rgb.data();
     const float* segs = st->segments.data();
+    const int cb = ct_blend();
 #pragma omp parallel for schedule(dynamic, 1)
     for (int t = 0; t < T; ++t) {
         const int tx = t % gx, ty = t / gx;
@@ -500,7 +561,7 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
                     const uint32_t g = st->point_list[k];
                     const float* co = &st->conic_opacity[4 * (size_t)g];
                     const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
-                    const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    const float power = blend_power(cb, co, dx, dy);
                     if (power > 0.0f) continue;
                     const float alpha = std::min(0.99f, co[3] * jitter_exp(oracle_exp(power), g, pix_id));
                     if (alpha < 1.0f / 255.0f) continue;
@@ -510,10 +571,17 @@ void* oracle_forward(const OracleSettings* sp, const OracleInputs* in, float* ou
                         break;
                     }
                     mix(contributor);
-                    for (int ch = 0; ch < NCH; ++ch) C[ch] += feat[g * NCH + ch] * alpha * Tr;
-                    weight += alpha * Tr;
-                    D += st->depths[g] * alpha * Tr;
-                    for (int c = 0; c < NCLS; ++c) S[c] += segs[g * NCLS + c] * alpha * Tr;
+                    if (!cb) {
+                        for (int ch = 0; ch < NCH; ++ch) C[ch] += feat[g * NCH + ch] * alpha * Tr;
+                        weight += alpha * Tr;
+                        D += st->depths[g] * alpha * Tr;
+                        for (int c = 0; c < NCLS; ++c) S[c] += segs[g * NCLS + c] * alpha * Tr;
+                    } else {  // forward.cu:362-366 under contraction: x += (f*alpha)*T -> fma
+                        for (int ch = 0; ch < NCH; ++ch) C[ch] = std::fma(feat[g * NCH + ch] * alpha, Tr, C[ch]);
+                        weight = std::fma(alpha, Tr, weight);
+                        D = std::fma(st->depths[g] * alpha, Tr, D);
+                        for (int c = 0; c < NCLS; ++c) S[c] = std::fma(segs[g * NCLS + c] * alpha, Tr, S[c]);
+                    }
                     Tr = test_T;
                     last_contributor = contributor;
                 }
@@ -592,6 +660,7 @@ int oracle_backward(void* h, const OracleInputs* in, const float* dL_dpix, const
     // the exact sum of the fp32 per-pixel terms is the centre of its outputs.
     std::vector<double> contrib((size_t)I * 12, 0.0), cabs((size_t)I * 12, 0.0);
     const float ddelx_dx = 0.5 * W, ddely_dy = 0.5 * H;
+    const int cb = ct_blend();
 
     // renderCUDA backward (backward.cu:414-639)
 #pragma omp parallel for schedule(dynamic, 1)
@@ -623,7 +692,7 @@ int oracle_backward(void* h, const OracleInputs* in, const float* dL_dpix, const
                     const uint32_t g = st->point_list[k];
                     const float* co = &st->conic_opacity[4 * (size_t)g];
                     const float dx = st->means2D[2 * g] - pfx, dy = st->means2D[2 * g + 1] - pfy;
-                    const float power = -0.5f * (co[0] * dx * dx + co[2] * dy * dy) - co[1] * dx * dy;
+                    const float power = blend_power(cb, co, dx, dy);
                     if (power > 0.0f) continue;
                     const float G = jitter_exp(oracle_exp(power), g, pix_id);
                     const float alpha = std::min(0.99f, co[3] * G);

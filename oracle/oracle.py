@@ -56,6 +56,9 @@ def lib():
         L.oracle_set_acc32.argtypes = [ctypes.c_int]
         L.oracle_set_exp_libm.argtypes = [ctypes.c_int]
         L.oracle_set_exp_jitter.argtypes = [ctypes.c_uint]
+        L.oracle_set_exp_jitter_ulps.argtypes = [ctypes.c_int]
+        L.oracle_set_contract.argtypes = [ctypes.c_int]
+        L.oracle_get_contract.restype = ctypes.c_int
         L.oracle_set_weight_sums.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
         L.oracle_expf.argtypes = [ctypes.c_float]
         L.oracle_expf.restype = ctypes.c_float
@@ -95,10 +98,28 @@ def set_exp_libm(on):
     lib().oracle_set_exp_libm(int(bool(on)))
 
 
-def set_exp_jitter(seed):
-    """seed != 0: every blend exp moves by -2 .. +2 ulp (hash of seed, Gaussian, pixel), the
-    same in forward and backward -- the reference algorithm under another faithful exp; 0: off."""
+def set_exp_jitter(seed, ulps=1):
+    """seed != 0: every blend exp moves by -ulps .. +ulps ulp (hash of seed, Gaussian, pixel),
+    the same in forward and backward -- the reference algorithm under another exp of that
+    accuracy around gsr_expf (CUDA's expf: 2 ulp); 0: off."""
+    lib().oracle_set_exp_jitter_ulps(int(ulps))
     lib().oracle_set_exp_jitter(int(seed))
+
+
+# nvcc contraction model (gsr_oracle.cpp "nvcc contraction model"): bit flags
+CT_PRE, CT_BLEND, CT_RIGHT = 1, 2, 4
+
+
+def set_contract(mode):
+    """0 (default): every a*b+c rounded twice, as gsr evaluates it.  CT_PRE: the projection,
+    ndc2Pix, cov3D, cov2D and the determinant / eigenvalue lines contracted into FMAs the way
+    nvcc's default --fmad=true does (LLVM DAG-combine rule, left product of two fused;
+    | CT_RIGHT: the right one); CT_BLEND: the blend's power and sums likewise."""
+    lib().oracle_set_contract(int(mode))
+
+
+def get_contract():
+    return int(lib().oracle_get_contract())
 
 
 def expf(x):

@@ -54,7 +54,7 @@ def run_gsr(scene, cam, device="cuda", bg=(0.0, 0.0, 0.0), scale_modifier=1.0, c
         I = _num_rendered(fn)
         res["num_rendered"] = I
         for name in ("tiles_touched", "rec", "clamped", "point_list", "ranges", "n_contrib_tiles", "goff", "bbase",
-                     "slot_vals", "tile_order", "order"):
+                     "tile_order", "order"):
             res[name] = _C.debug_state(name, P, W, H, I, geom, binning, img).cpu().numpy()
         res["n_contrib"] = untile_n_contrib(res["n_contrib_tiles"], W, H)
     if grads is not None:

@@ -1,31 +1,36 @@
-"""Parity against an INDEPENDENT exp, stated precisely (VERDICT r4 Next #5).
+"""Parity against an INDEPENDENT exp, stated precisely (VERDICT r4 Next #5, r5 Next #1).
 
 The HIP path blends with gsr_expf, which the CPU oracle shares bit for bit, so every other
 parity test compares identical exps.  The reference's CUDA expf (forward.cu:351,
-backward.cu:547; specified at 2 ulp) cannot run here; the closest stand-in is the oracle
-blending with the C library's expf (glibc).  Two faithful exps differ in the last bit on a
-fraction of inputs, and that difference reaches the outputs through exactly two mechanisms,
-which this test separates and bounds:
+backward.cu:547) is specified at 2 ulp and cannot run here.  Three stand-ins for it, each a
+mode of the oracle ("L" below):
+  * libm: the C library's expf (glibc: < 1 ulp, almost always correctly rounded);
+  * jit1 / jit2: gsr_expf moved by -1..+1 / -2..+2 ulp per (Gaussian, pixel) by a fixed hash
+    (oracle set_exp_jitter), the same in forward and backward -- an exp of CUDA's specified
+    accuracy, and a wider perturbation than glibc's.
+Two exps that differ in the last bits reach the outputs through exactly two mechanisms, which
+this test separates and bounds:
 
 1. Flipped blend decisions.  alpha >= 1/255 and T(1 - alpha) >= 1e-4 (forward.cu:352-359)
    are thresholds: a last-bit alpha can change which list positions a pixel blends or where it
    stops.  The oracle hashes every pixel's decision sequence (oracle_get "dhash": the blended
    positions and the terminating one); pixels whose hash differs between the two exps are
-   the flipped pixels.  They are counted and reported (0 or 1 per view at these configs);
+   the flipped pixels.  They are counted and reported (0-5 per view at these configs);
    everything below is asserted on the other pixels (a flipped pixel's upstream gradients
    are zeroed, which removes its every gradient term).
 2. The backward's T_final recovery.  backward.cu:468 starts each pixel's back-to-front replay
    from T_final = 1 - (weight sum) and divides by (1 - alpha) per contributor.  A weight sum
    that differs in its last bits (|d alpha_out| <= 1e-6 here) becomes a relative error of
    ~1e-7 / T_final in every T the replay reconstructs; dense scenes have T_final < 1e-3 on
-   most pixels, so 0.1-1 % of gradient elements of the reference itself move by more than
+   most pixels, so 0.1-15 % of gradient elements of the reference itself move by more than
    1e-5 of the tensor maximum when only the exp changes (measured below, "unpinned").
-   Running the libm backward from the HIP forward's weight sums (oracle set_weight_sums)
+   Running L's backward from the HIP forward's weight sums (oracle set_weight_sums)
    removes exactly this mechanism.
 
 Asserted per case (c1, sh3, a screen-filling 'large' case, and the BASELINE configs C2, the
-metric scene, C3 and C5 at full size), with G = the oracle with gsr_expf, L = the oracle with
-libm expf run from G's weight sums (mechanism 2 pinned), both on the unflipped pixels:
+metric scene, C3 and C5 at full size) and per exp mode, with G = the oracle with gsr_expf,
+L = the oracle in that mode run from G's weight sums (mechanism 2 pinned), both on the
+unflipped pixels:
   * point_list / num_rendered bit-exact (binning involves no exp);
   * n_contrib identical on every unflipped pixel; flipped pixels <= 1e-4 of the image;
   * images within 1e-5 * max(1, |ref|) on unflipped pixels, and the weight sums within 1e-6;
@@ -34,8 +39,9 @@ libm expf run from G's weight sums (mechanism 2 pinned), both on the unflipped p
       (i)   HIP vs G: 1e-5 -- the fp32 summation-order noise test_gpu_parity.py bounds;
       (ii)  G vs L: 1e-5 -- the exp's direct effect once mechanisms 1 and 2 are removed;
       (iii) HIP vs L: 2e-5 -- (i) + (ii), so nothing is left unexplained;
-  * the unpinned deviation (L from its own weight sums) is reported per tensor, with a 1e-3
-    regression guard on its maximum.
+  * the unpinned deviation (L from its own weight sums) is reported per tensor, with a
+    regression guard of about 1.5x the worst value measured over the seven cases in that mode
+    (profiles/round6_exp_modes.txt: libm 6.0e-4 -> guard 9e-4; jitter 1.1e-3 -> 1.7e-3).
 """
 import math
 
@@ -44,21 +50,22 @@ import pytest
 import torch
 
 import harness as Hn
-from gsr_tools.scene import config_scene_and_camera, synthetic_scene, orbit_camera
+from contract_cases import case_scene
 
 pytestmark = pytest.mark.gpu
 
 CASES = ["c1", "sh3", "large", "c2", "mt", "c3", "c5"]
+MODES = ["libm", "jit1", "jit2"]
 KEYS = ("dmeans2D", "dopacity", "dmeans3D", "dsh", "dscales", "drot", "dsegments")
+JITTER_SEED = 12345
+# unpinned guard per mode: ~1.5x the worst measured (profiles/round6_exp_modes.txt)
+UNPINNED_GUARD = {"libm": 9e-4, "jit1": 1.7e-3, "jit2": 1.7e-3}
 
 
-def _case(name):
-    if name == "sh3":
-        return synthetic_scene(20000, sh_degree=3, seed=3), orbit_camera(1, 333, 250, 300.0)
-    if name == "large":  # 400 screen-filling Gaussians: every pixel sees ~100 of them
-        return (synthetic_scene(400, sh_degree=2, seed=9, log_scale=math.log(0.4), log_scale_std=0.3),
-                orbit_camera(3, 300, 200, 250.0))
-    return config_scene_and_camera(name)
+def _set_mode(O, mode):
+    O.set_exp_libm(mode == "libm")
+    jit = mode.startswith("jit")
+    O.set_exp_jitter(JITTER_SEED if jit else 0, ulps=int(mode[3:]) if jit else 1)
 
 
 def _normwise(a, b, k):
@@ -68,17 +75,18 @@ def _normwise(a, b, k):
     return np.abs(a - b) / max(float(np.abs(b).max()), 1e-30)
 
 
+@pytest.mark.parametrize("mode", MODES)
 @pytest.mark.parametrize("name", CASES)
-def test_independent_exp_precise(gpu_available, oracle_mod, name):
+def test_independent_exp_precise(gpu_available, oracle_mod, name, mode):
     O = oracle_mod
-    scene, cam = _case(name)
+    scene, cam = case_scene(name)
     H, W = cam.height, cam.width
     grads = Hn.upstream_grads(H, W)
     # decisions under both exps (forward only for gsr_expf: the HIP path's decisions are the
     # oracle's bit for bit, tests/test_gpu_parity.py)
-    O.set_exp_libm(False)
+    _set_mode(O, "none")
     own = O.run_scene(scene, cam)
-    O.set_exp_libm(True)
+    _set_mode(O, mode)
     try:
         lib = O.run_scene(scene, cam)
         flipped = (own.get("dhash") != lib.get("dhash")).reshape(H, W)
@@ -103,7 +111,7 @@ def test_independent_exp_precise(gpu_available, oracle_mod, name):
         lib.set_weight_sums(own.alpha)           # ... and from gsr_expf's (mechanism 2 pinned)
         pinned = lib.backward(*ups)
     finally:
-        O.set_exp_libm(False)
+        _set_mode(O, "none")
     G = own.backward(*ups)
     del own
     checks = {"(i) HIP vs G": (g["grads"], G, 1e-5), "(ii) G vs L": (G, pinned, 1e-5),
@@ -117,13 +125,13 @@ def test_independent_exp_precise(gpu_available, oracle_mod, name):
             rep[c][k] = (int((e > tol).sum()), float(e.max()))
         f = _normwise(g["grads"][k], free[k], k)
         rep_free[k] = (float((f > 1e-5).mean()), float(f.max()))
-    print(f"\n{name}: flipped pixels {int(flipped.sum())} of {flipped.size}; image (unflipped) {img:.1e}; "
+    print(f"\n{name} [{mode}]: flipped pixels {int(flipped.sum())} of {flipped.size}; image (unflipped) {img:.1e}; "
           f"|d weight sum| {dw:.1e}")
     for c, r in rep.items():
         print(f"  {c:15s} (tol {checks[c][2]:.0e}): " + ", ".join(f"{k} {n} (max {m:.1e})" for k, (n, m) in r.items()))
-    print("  unpinned HIP vs libm: " + ", ".join(f"{k} {fr:.2%} > 1e-5 (max {m:.1e})" for k, (fr, m) in rep_free.items()))
+    print(f"  unpinned HIP vs {mode}: " + ", ".join(f"{k} {fr:.2%} > 1e-5 (max {m:.1e})" for k, (fr, m) in rep_free.items()))
     for c, r in rep.items():
         for k, (n, m) in r.items():
             assert n == 0, f"{c}: {k}: {n} elements above {checks[c][2]:.0e} * max|ref| (max {m:.2e})"
     for k, (fr, m) in rep_free.items():
-        assert m <= 1e-3, f"{k}: unpinned max normwise deviation {m:.2e}"
+        assert m <= UNPINNED_GUARD[mode], f"{k}: unpinned max normwise deviation {m:.2e}"

@@ -293,3 +293,35 @@ def test_multiview_forward_streams(gpu_available, streams, monkeypatch):
     scene = synthetic_scene(4000, sh_degree=3, seed=48)
     d = _leaves(scene)
     _check(d, _views(5, 3))
+
+
+def test_multiview_forward_end_failure_frees_tickets(gpu_available, monkeypatch):
+    """an error while ending view v of a multi-view forward (e.g. an out-of-memory
+    stage-B buffer after gsr_forward_wait) must still end views v+1.. (their deferred tickets
+    are per-thread pinned slots, 16 of them) and join the side streams.  Ten failed batches of
+    four views would leak 20 tickets without that; a batch after them must still work."""
+    from diff_gaussian_rasterization import _C
+    import diff_gaussian_rasterization as dgr
+    scene = synthetic_scene(6000, sh_degree=3, seed=49)
+    d = _leaves(scene)
+    views = _views(4, 3)
+    real_end = _C.rasterize_gaussians_end
+    calls = {"n": 0}
+
+    def failing_end(h):
+        out = real_end(h)
+        calls["n"] += 1
+        if calls["n"] % 4 == 2:
+            raise RuntimeError("injected failure after the wait")
+        return out
+
+    _multi(d, views)  # warm the binning guess so that begin() defers
+    monkeypatch.setattr(_C, "rasterize_gaussians_end", failing_end)
+    for _ in range(10):
+        calls["n"] = 0
+        with pytest.raises(RuntimeError, match="injected"):
+            dgr.rasterize_gaussians_multiview(d["means3D"], [torch.zeros_like(d["means3D"]) for _ in views],
+                                              raster_settings_list=[st for st, _ in views], **_kw(d))
+    monkeypatch.setattr(_C, "rasterize_gaussians_end", real_end)
+    torch.cuda.synchronize()
+    _check(d, views)

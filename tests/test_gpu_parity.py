@@ -343,6 +343,33 @@ def test_rows_binning_matches_radix_path(gpu_available, case):
         np.testing.assert_array_equal(ga[k], gb[k], err_msg=k)
 
 
+@pytest.mark.parametrize("route", ["histogram_blocks", "standalone"])
+def test_block_bases_multi_segment(gpu_available, route):
+    """the record-slot block bases (binning.hip block_bases) are computed in segments
+    of BB_SEG = 2048 block totals (524,288 Gaussians); segment k adds the carry of the earlier
+    ones.  1.2M Gaussians give three segments.  Both launch routes are pinned directly against a
+    numpy scan: the extra blocks of the depth sort's histogram kernel (look-back / grouped sort,
+    the default) and the standalone k_block_bases (table-driven depth sort: look-back off)."""
+    from diff_gaussian_rasterization import _C
+    scene, cam = synthetic_scene(1_200_000, sh_degree=0, seed=50), orbit_camera(1, 320, 240, 300.0)
+    try:
+        if route == "standalone":
+            _C.set_option("sort_lookback_max", 0)
+        g = Hn.run_gsr(scene, cam)
+    finally:
+        _C.set_option("sort_lookback_max", 4 << 20)
+    tt = g["tiles_touched"].astype(np.int64)
+    blk_starts = np.arange(0, tt.size, 256)
+    blk = np.add.reduceat(tt, blk_starts)
+    assert blk.size > 2 * 2048, "fewer than three block-base segments"
+    want_bbase = np.concatenate([[0], np.cumsum(blk)[:-1]])
+    excl = np.cumsum(tt) - tt
+    want_goff = excl - np.repeat(excl[blk_starts], np.diff(np.append(blk_starts, tt.size)))
+    np.testing.assert_array_equal(g["bbase"].astype(np.int64), want_bbase, err_msg="bbase")
+    np.testing.assert_array_equal(g["goff"].astype(np.int64), want_goff, err_msg="goff")
+    assert int(blk.sum()) == g["num_rendered"] > 0
+
+
 def _tile_queue(state, T):
     """The render schedule after the T-entry tile order (gsr_internal.h TileSched): sched words,
     bucket counts, bucket lists (2T entries each: tile | kind << 30; the debug copy is int32, so

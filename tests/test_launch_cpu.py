@@ -15,10 +15,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG = os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd")
 
 CHILD = textwrap.dedent("""
-    import json, os, sys
+    import json, os, sys, time
     import torch, torch.distributed as dist
-    dist.init_process_group("gloo")
+    sys.path.insert(0, os.environ["PKG"])
+    from gsr_tools.launch import dist_timeout
+    dist.init_process_group("gloo", timeout=dist_timeout())
     r, w = dist.get_rank(), dist.get_world_size()
+    if os.environ.get("SLEEP_RANK") == str(r):
+        time.sleep(600)                     # never joins the collective below
+
     assert os.environ["LOCAL_RANK"] == str(r) and os.environ["MASTER_ADDR"] == "127.0.0.1"
     fail = os.environ.get("FAIL_RANK")
     if fail is not None and int(fail) == r:
@@ -30,6 +35,8 @@ CHILD = textwrap.dedent("""
         print(json.dumps({"world": w, "sum": t.item(), "launcher": os.environ.get("GSR_LAUNCHER")}))
     dist.barrier()
     dist.destroy_process_group()
+    if os.environ.get("LINGER_RANK") == str(r):
+        time.sleep(600)                     # finishes its work, then never exits
 """)
 
 PARENT = textwrap.dedent("""
@@ -38,6 +45,7 @@ PARENT = textwrap.dedent("""
     from gsr_tools import launch
     assert launch.needs_launch(int(sys.argv[1]))
     sys.exit(launch.spawn_ranks(int(sys.argv[1]), [sys.executable, sys.argv[2]], grace_s=3.0,
+                                straggler_s=float(os.environ.get("STRAGGLER_S", "60")),
                                 env=dict(os.environ, GSR_LAUNCHER="test")))
 """)
 
@@ -48,6 +56,7 @@ def _run(tmp_path, world, extra_env=None):
     parent = tmp_path / "parent.py"
     parent.write_text(PARENT.format(pkg=PKG))
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["PKG"] = PKG
     env.update(extra_env or {})
     return subprocess.run([sys.executable, str(parent), str(world), str(child)], env=env, capture_output=True,
                           text=True, timeout=180)
@@ -70,6 +79,30 @@ def test_spawn_ranks_propagates_failure(tmp_path):
     p = _run(tmp_path, 2, {"FAIL_RANK": "1"})
     assert p.returncode == 3, (p.returncode, p.stderr[-2000:])
     assert "rank 1 exited with status 3" in p.stderr
+
+
+def test_rank_stuck_in_collective_fails_fast(tmp_path):
+    """VERDICT r5 Next #7: one rank sleeps instead of joining a collective.  The others' gloo
+    all_reduce times out after GSR_DIST_TIMEOUT_S (bench.py passes the same dist_timeout() to
+    init_process_group), they exit non-zero, and the launcher terminates the sleeper after its
+    grace period: the job ends non-zero within the timeout, not at the driver's limit."""
+    import time
+    t0 = time.monotonic()
+    p = _run(tmp_path, 2, {"SLEEP_RANK": "1", "GSR_DIST_TIMEOUT_S": "5"})
+    took = time.monotonic() - t0
+    assert p.returncode != 0, p.stderr[-2000:]
+    assert "terminating rank 1" in p.stderr
+    assert took < 60, took
+
+
+def test_rank_outliving_the_job_is_terminated(tmp_path):
+    """A rank that keeps running long after another exited 0 (straggler grace) is terminated
+    and the job exits with launch.STRAGGLER_STATUS."""
+    sys.path.insert(0, PKG)
+    from gsr_tools import launch
+    p = _run(tmp_path, 2, {"LINGER_RANK": "1", "STRAGGLER_S": "3"})
+    assert p.returncode == launch.STRAGGLER_STATUS, (p.returncode, p.stderr[-2000:])
+    assert "still running" in p.stderr and "terminating rank 1" in p.stderr
 
 
 def test_needs_launch():
