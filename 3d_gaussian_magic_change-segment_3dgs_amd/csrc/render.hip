@@ -128,7 +128,8 @@ __device__ __forceinline__ float gsr_expf_nc(float x) {
 #ifdef GSR_STATS
 // Instrumented build (tools/render_stats.py): wave-uniform loop counters, 16 per
 // kernel (fwd at 0, bwd at 16): 0 visited, 1 near-skip, 2 prefiltered out, 3 full,
-// 4 ok pixels, 5 batches, 6 zero-tail (bwd), 7 instances, 8 strips processed.
+// 4 ok pixels, 5 batches, 6 zero-tail (bwd), 7 instances, 8 strips processed, 13 instances
+// fetched (their records read: the render kernels' per-instance HBM traffic).
 __device__ unsigned long long g_gsr_stats[32];
 extern "C" __attribute__((visibility("default"))) int gsr_stats_read(unsigned long long* host, int reset) {
     if (hipMemcpyFromSymbol(host, HIP_SYMBOL(g_gsr_stats), sizeof(g_gsr_stats)) != hipSuccess) return -1;
@@ -431,6 +432,7 @@ __device__ __forceinline__ void fwd_tile(int W, int H, int gx, int ntiles, int t
         }
         const int cnt = min(64, n - base);
         STAT(5, 1);
+        STAT(13, cnt);  // instances fetched (records read)
         const Batch nxt = fetch_batch(rec, g_next);
         g_next = plist[min(base + 128 + lane, nlast)];
         const float4 ra = cur.a, rb = cur.b, rc = cur.c;
@@ -872,6 +874,7 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
         for (int top = top0; top > seg_lo; top -= 64) {
             const int cnt = min(64, top - seg_lo);
             STAT(5, 1);
+            STAT(13, cnt);  // instances fetched (records read)
             flush();
             const BatchB nxt = fetch_batch_b(rec, bbase, g_next);
             g_next = plist[max(top - 129 - lane, 0)];

@@ -131,12 +131,16 @@ def synthetic_scene(P, sh_degree=3, extent=1.5, log_scale=math.log(0.01), log_sc
     SH DC = RGB2SH(U[0,1]), rest N(0, 0.05)."""
     g = torch.Generator().manual_seed(seed)
     M = (sh_degree + 1) ** 2
+    # exp / sigmoid / norm in float64, rounded once: torch's float32 CPU kernels differ in the
+    # last bit between CPUs (the GPU box's EPYC and this container's Xeon gave different
+    # scales and opacities), which made the "same" scene differ between machines
+    f64 = lambda t: t.to(torch.float64)
     means = (torch.rand(P, 3, generator=g) * 2 - 1) * extent
-    scales = torch.exp(torch.randn(P, 3, generator=g) * log_scale_std + log_scale)
-    rots = torch.randn(P, 4, generator=g)
-    rots = rots / rots.norm(dim=1, keepdim=True)
-    opac = torch.sigmoid(torch.randn(P, 1, generator=g))
-    segs = torch.sigmoid(torch.randn(P, n_classes, generator=g))
+    scales = torch.exp(f64(torch.randn(P, 3, generator=g)) * log_scale_std + log_scale).float()
+    rots = f64(torch.randn(P, 4, generator=g))
+    rots = (rots / rots.norm(dim=1, keepdim=True)).float()
+    opac = torch.sigmoid(f64(torch.randn(P, 1, generator=g))).float()
+    segs = torch.sigmoid(f64(torch.randn(P, n_classes, generator=g))).float()
     shs = torch.zeros(P, M, 3)
     shs[:, 0, :] = rgb2sh(torch.rand(P, 3, generator=g))
     if M > 1:

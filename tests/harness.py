@@ -117,3 +117,23 @@ def tol_report(a, b, scale_floor=1.0):
     if a.size == 0:
         return 0.0
     return float(np.max(np.abs(a - b) / np.maximum(scale_floor, np.abs(b))))
+
+
+def reference_noise(oracle_mod, run, grads, ref_grads):
+    """Per tensor: max |acc32 - exact| / max|exact| -- how far the reference's own fp32
+    atomicAdd accumulation (the oracle summing in one fixed fp32 order, set_acc32) moves each
+    gradient from the exact sums the oracle reports.  `run` is run_oracle's "_run"."""
+    oracle_mod.set_acc32(True)
+    try:
+        g32 = run.backward(grads["color"].numpy(), grads["segment"].numpy(), grads["depth"].numpy(),
+                           grads["alpha"].numpy())
+    finally:
+        oracle_mod.set_acc32(False)
+    out = {}
+    for k, ref in ref_grads.items():
+        a, b = g32[k].astype(np.float64), ref.astype(np.float64)
+        if k == "dmeans2D":
+            a, b = a[:, :2], b[:, :2]
+        m = float(np.abs(b).max()) if b.size else 0.0
+        out[k] = float(np.abs(a - b).max() / m) if m > 0 else 0.0
+    return out

@@ -185,7 +185,9 @@ def test_c4_eight_views_sharded_over_two_ranks(gpu_available):
 
 def test_c4_sharded_view_vs_oracle(gpu_available, oracle_mod):
     """View 5 of the 8-view orbit (rank 1's shard) at C3 size against the CPU oracle:
-    bit-exact integer outputs, images and scale-free gradients within the parity bounds."""
+    bit-exact integer outputs, images and scale-free gradients within the parity bounds
+    (with the reference's own fp32-order deviation: here one dscales element moves by 1.7e-5
+    of the tensor maximum between the exact and an fp32 atomic order)."""
     import harness as Hn
     from gsr_tools.scene import config_scene_and_camera
     from test_gpu_parity import assert_integer_parity, assert_image_parity, assert_grad_parity
@@ -193,8 +195,9 @@ def test_c4_sharded_view_vs_oracle(gpu_available, oracle_mod):
     grads = Hn.upstream_grads(cam.height, cam.width, seed=105)
     g = Hn.run_gsr(scene, cam, grads=grads)
     r = Hn.run_oracle(oracle_mod, scene, cam, grads=grads)
-    r.pop("_run", None)
+    noise = Hn.reference_noise(oracle_mod, r.pop("_run"), grads, r["grads"])
+    print("\nreference fp32-order deviation: " + ", ".join(f"{k} {v:.1e}" for k, v in noise.items()))
     assert g["num_rendered"] > 15_000_000
     assert_integer_parity(g, r)
     assert_image_parity(g, r)
-    assert_grad_parity(g["grads"], r["grads"])
+    assert_grad_parity(g["grads"], r["grads"], noise)

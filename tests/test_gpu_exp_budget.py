@@ -36,12 +36,19 @@ unflipped pixels:
   * images within 1e-5 * max(1, |ref|) on unflipped pixels, and the weight sums within 1e-6;
   * gradients, scale-free (|d| <= tol * max|ref| per element of each tensor, as
     test_gpu_parity.py), ZERO elements above:
-      (i)   HIP vs G: 1e-5 -- the fp32 summation-order noise test_gpu_parity.py bounds;
-      (ii)  G vs L: 1e-5 -- the exp's direct effect once mechanisms 1 and 2 are removed;
-      (iii) HIP vs L: 2e-5 -- (i) + (ii), so nothing is left unexplained;
+      (i)   HIP vs G: 1e-5 -- the fp32 summation-order noise test_gpu_parity.py bounds
+            (dscales / drot: 4e-5, below);
+      (ii)  G vs L: 1e-5 -- the exp's direct effect once mechanisms 1 and 2 are removed --
+            except dscales / drot: 4e-5.  Those two leave the per-Gaussian chain
+            dconic -> dcov2D -> dcov3D -> (scale, rotation) (backward.cu:141-341), whose
+            cancellations amplify a last-bit change of the summed conic gradient: measured
+            (profiles/round6_exp_modes.txt) every other tensor stays below 1e-6 in every mode,
+            dscales / drot reach 0.8e-5 (libm) to 2.7e-5 (+-2 ulp) at C3 / C5;
+      (iii) HIP vs L: (i) + (ii), so nothing is left unexplained;
   * the unpinned deviation (L from its own weight sums) is reported per tensor, with a
     regression guard of about 1.5x the worst value measured over the seven cases in that mode
-    (profiles/round6_exp_modes.txt: libm 6.0e-4 -> guard 9e-4; jitter 1.1e-3 -> 1.7e-3).
+    (profiles/round6_exp_modes.txt, worst at the 'large' case: libm 3.4e-4 -> guard 5.5e-4;
+    jitter 1.5e-3 -> 2.3e-3; round 5's single guard was 1e-3).
 """
 import math
 
@@ -58,8 +65,13 @@ CASES = ["c1", "sh3", "large", "c2", "mt", "c3", "c5"]
 MODES = ["libm", "jit1", "jit2"]
 KEYS = ("dmeans2D", "dopacity", "dmeans3D", "dsh", "dscales", "drot", "dsegments")
 JITTER_SEED = 12345
+# dscales / drot: 4e-5 -- the cancellations of the dconic -> dcov3D -> (scale, rotation) chain
+# (backward.cu:141-341) move them most: the reference's own fp32 atomic-order deviation reaches
+# 1.7e-5 of the tensor maximum there at C3 (tests/test_gpu_parity.py assert_grad_parity)
+TOL_I = {k: (4e-5 if k in ("dscales", "drot") else 1e-5) for k in KEYS}
+TOL_II = {k: (4e-5 if k in ("dscales", "drot") else 1e-5) for k in KEYS}
 # unpinned guard per mode: ~1.5x the worst measured (profiles/round6_exp_modes.txt)
-UNPINNED_GUARD = {"libm": 9e-4, "jit1": 1.7e-3, "jit2": 1.7e-3}
+UNPINNED_GUARD = {"libm": 5.5e-4, "jit1": 2.3e-3, "jit2": 2.3e-3}
 
 
 def _set_mode(O, mode):
@@ -114,24 +126,25 @@ def test_independent_exp_precise(gpu_available, oracle_mod, name, mode):
         _set_mode(O, "none")
     G = own.backward(*ups)
     del own
-    checks = {"(i) HIP vs G": (g["grads"], G, 1e-5), "(ii) G vs L": (G, pinned, 1e-5),
-              "(iii) HIP vs L": (g["grads"], pinned, 2e-5)}
+    checks = {"(i) HIP vs G": (g["grads"], G, TOL_I), "(ii) G vs L": (G, pinned, TOL_II),
+              "(iii) HIP vs L": (g["grads"], pinned, {k: TOL_I[k] + v for k, v in TOL_II.items()})}
     rep, rep_free = {c: {} for c in checks}, {}
     for k in KEYS:
         if k not in g["grads"]:
             continue
         for c, (x, y, tol) in checks.items():
+            t = tol[k] if isinstance(tol, dict) else tol
             e = _normwise(x[k], y[k], k)
-            rep[c][k] = (int((e > tol).sum()), float(e.max()))
+            rep[c][k] = (int((e > t).sum()), float(e.max()), t)
         f = _normwise(g["grads"][k], free[k], k)
         rep_free[k] = (float((f > 1e-5).mean()), float(f.max()))
     print(f"\n{name} [{mode}]: flipped pixels {int(flipped.sum())} of {flipped.size}; image (unflipped) {img:.1e}; "
           f"|d weight sum| {dw:.1e}")
     for c, r in rep.items():
-        print(f"  {c:15s} (tol {checks[c][2]:.0e}): " + ", ".join(f"{k} {n} (max {m:.1e})" for k, (n, m) in r.items()))
+        print(f"  {c:15s}: " + ", ".join(f"{k} {n} > {t:.0e} (max {m:.1e})" for k, (n, m, t) in r.items()))
     print(f"  unpinned HIP vs {mode}: " + ", ".join(f"{k} {fr:.2%} > 1e-5 (max {m:.1e})" for k, (fr, m) in rep_free.items()))
     for c, r in rep.items():
-        for k, (n, m) in r.items():
-            assert n == 0, f"{c}: {k}: {n} elements above {checks[c][2]:.0e} * max|ref| (max {m:.2e})"
+        for k, (n, m, t) in r.items():
+            assert n == 0, f"{c}: {k}: {n} elements above {t:.0e} * max|ref| (max {m:.2e})"
     for k, (fr, m) in rep_free.items():
         assert m <= UNPINNED_GUARD[mode], f"{k}: unpinned max normwise deviation {m:.2e}"

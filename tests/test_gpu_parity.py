@@ -51,7 +51,16 @@ def assert_image_parity(g, r):
         assert err.max() <= IMG_OUTLIER_MAX, f"{k}: max err {err.max():.3e}"
 
 
-def assert_grad_parity(g, r):
+NOISE_FACTOR = 4.0  # x the reference's own fp32 atomic-order deviation (see assert_grad_parity)
+
+
+def assert_grad_parity(g, r, noise=None):
+    """Scale-free gradient parity.  noise (tensor -> the reference's own fp32-order deviation
+    from the exact sums, Hn.reference_noise): where the reference itself moves an element by
+    more than 1e-5 of the tensor maximum between two atomic orders -- dscales / drot at the
+    full-size configs, through the cancellations of the dconic -> dcov3D -> (scale, rotation)
+    chain (backward.cu:141-341) -- the bound is NOISE_FACTOR times that deviation (the
+    precedent of test_single_gaussian_small_image)."""
     for k, ref in r.items():
         if k not in g:
             continue
@@ -64,9 +73,10 @@ def assert_grad_parity(g, r):
             assert not np.any(a), f"{k}: reference is all zero, gsr max |g| = {np.abs(a).max():.3e}"
             continue
         err = np.abs(a - b) / scale
-        frac = float((err > GRAD_TOL).mean()) if err.size else 0.0
-        assert frac <= GRAD_OUTLIER_FRAC, f"{k}: {frac:.2e} of elements above {GRAD_TOL} (max {err.max():.3e})"
-        assert (err.max() if err.size else 0.0) <= GRAD_OUTLIER_MAX, f"{k}: max normwise err {err.max():.3e}"
+        tol = max(GRAD_TOL, NOISE_FACTOR * noise[k]) if noise and k in noise else GRAD_TOL
+        frac = float((err > tol).mean()) if err.size else 0.0
+        assert frac <= GRAD_OUTLIER_FRAC, f"{k}: {frac:.2e} of elements above {tol:.2e} (max {err.max():.3e})"
+        assert (err.max() if err.size else 0.0) <= max(GRAD_OUTLIER_MAX, tol), f"{k}: max normwise err {err.max():.3e}"
 
 
 def compare(oracle_mod, scene, cam, **kw):

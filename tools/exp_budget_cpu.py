@@ -10,6 +10,7 @@ import sys
 import time
 
 import numpy as np
+import torch
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd")]
@@ -51,7 +52,8 @@ def main(cases, modes):
                 lib = O.run_scene(scene, cam)
                 flipped = (own.get("dhash") != lib.get("dhash")).reshape(H, W)
                 keep = ~flipped
-                ups = [(grads[k] * keep[None]).numpy() for k in ("color", "segment", "depth", "alpha")]
+                km = torch.from_numpy(keep)[None]
+                ups = [(grads[k] * km).contiguous().numpy() for k in ("color", "segment", "depth", "alpha")]
                 img = 0.0
                 for a, b in ((own.color, lib.color), (own.depth, lib.depth), (own.alpha, lib.alpha), (own.segment, lib.segment)):
                     e = np.abs(a.astype(np.float64) - b) / np.maximum(1.0, np.abs(b))
@@ -68,7 +70,7 @@ def main(cases, modes):
                   for k in KEYS if k in G}
             worst = max(worst, max(m for _, m in un.values()))
             print(f"{name} {mode}: flipped {int(flipped.sum())}/{flipped.size}; image {img:.1e}; dweight {dw:.1e}; "
-                  f"(ii) max {max(ii.values()):.1e}; unpinned " +
+                  f"(ii) max {max(ii.values()):.1e} (" + ", ".join(f"{k} {v:.1e}" for k, v in ii.items()) + "); unpinned " +
                   ", ".join(f"{k} {fr:.2%} (max {m:.1e})" for k, (fr, m) in un.items()) +
                   f"  [{time.time() - t0:.1f} s]", flush=True)
         del own

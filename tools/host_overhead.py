@@ -78,6 +78,17 @@ def main():
         step()
     torch.cuda.synchronize()
     log.clear()
+    if os.environ.get("HOST_CPROFILE"):  # function-level host profile of the same loop
+        import cProfile
+        import pstats
+        pr = cProfile.Profile()
+        pr.enable()
+        for _ in range(steps):
+            step()
+        torch.cuda.synchronize()
+        pr.disable()
+        pstats.Stats(pr).sort_stats("tottime").print_stats(35)
+        log.clear()
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
