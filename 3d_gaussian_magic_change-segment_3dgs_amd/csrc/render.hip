@@ -1074,7 +1074,8 @@ __device__ __forceinline__ void bwd_tile(int W, int H, int gx, int tile, int s0,
     replay();
     flush();
     STAT_FLUSH(16)
-    WT_END(1, wslot, tile, n, top0, NS)
+    // mode: strips | 16 front segment | 32 back segment (from seg_lo = ck)
+    WT_END(1, wslot, tile, n, top0, NS | (seg_hi < 0x7fffffff ? 16 : 0) | (seg_lo > 0 ? 32 : 0))
 }
 
 #if GSR_RENDER_PART != 1

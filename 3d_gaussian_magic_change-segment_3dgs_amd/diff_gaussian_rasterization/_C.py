@@ -227,6 +227,9 @@ def _dev_f32(t, device, name, align=4):
 
 
 _BIN_GUESS = os.environ.get("GSR_BIN_GUESS", "1") != "0"
+# the single-view host work in C++ when built (_host.py; None: this module's ctypes route)
+from . import _host  # noqa: E402
+_HOST = _host.load()
 _last_rendered = {}  # device -> num_rendered of the recent forwards (binning size guess)
 _GUESS_WINDOW = 16   # a trainer cycling through a batch of views sees each view's count again
 
@@ -261,11 +264,34 @@ def _check_segments(segments, P):
         raise RuntimeError(f"segments must have shape (num_points, {NUM_CLASS}) (reference config.h:16 NUM_CLASS)")
 
 
+def _guess(device):
+    """Binning capacity guess for the next forward on `device`: the largest of the recent
+    counts + 15% (0: none)."""
+    recent = _last_rendered.get(device)
+    cap = max(recent) if recent else 0
+    return cap + cap // 7 + 4096 if cap and _BIN_GUESS else 0
+
+
+def _record(device, num_rendered):
+    recent = _last_rendered.setdefault(device, [])
+    recent.append(num_rendered)
+    del recent[:-_GUESS_WINDOW]
+
+
 def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, rotations, scale_modifier,
                         cov3D_precomp, viewmatrix, projmatrix, tan_fovx, tan_fovy, image_height, image_width, sh,
                         degree, campos, prefiltered, debug):
     """RasterizeGaussiansCUDA (DGR/rasterize_points.cu:35-125).
     Returns (num_rendered, color, depth, segment, alpha, radii, geomBuffer, binningBuffer, imgBuffer)."""
+    if _HOST is not None:  # the same work in C++ (csrc/host_ext.cpp)
+        device = means3D.device
+        out = _HOST.rasterize_gaussians(background, means3D, colors, segments, opacity, scales, rotations,
+                                        float(scale_modifier), cov3D_precomp, viewmatrix, projmatrix, float(tan_fovx),
+                                        float(tan_fovy), int(image_height), int(image_width), sh, int(degree), campos,
+                                        bool(prefiltered), bool(debug), _guess(device))
+        if means3D.size(0) > 0:
+            _record(device, out[0])
+        return out
     return rasterize_gaussians_end(_forward_begin(False, background, means3D, colors, segments, opacity, scales,
                                                   rotations, scale_modifier, cov3D_precomp, viewmatrix, projmatrix,
                                                   tan_fovx, tan_fovy, image_height, image_width, sh, degree, campos,
@@ -336,9 +362,7 @@ def _forward_begin(deferred, background, means3D, colors, segments, opacity, sca
         # before it so that nothing but the render launches sits between the sync and the
         # GPU.  The largest, not the last: consecutive calls of a multi-view batch render
         # different views, and a guess below the count costs an exact re-run of stage B.
-        recent = _last_rendered.get(device)
-        cap = max(recent) if recent else 0
-        cap = cap + cap // 7 + 4096 if cap and _BIN_GUESS else 0
+        cap = _guess(device)
         binning = torch.empty(_lib.gsr_binning_bytes(cap), **u8) if cap else None
         # every call on a binning buffer uses the layout of its capacity (gsr.h); with a guess
         # gsr_forward runs stage B speculatively right behind stage A
@@ -379,9 +403,7 @@ def rasterize_gaussians_end(h):
             num_rendered = int(nr.value)
         else:
             rc, num_rendered = h["rc"], h["num_rendered"]
-        recent = _last_rendered.setdefault(device, [])
-        recent.append(num_rendered)
-        del recent[:-_GUESS_WINDOW]
+        _record(device, num_rendered)
         binning = h["binning"]
         if rc == GSR_NEED_BINNING:  # no guess, or too small: stage B with the exact size
             binning = torch.empty(_lib.gsr_binning_bytes(num_rendered), dtype=torch.uint8, device=device)
@@ -449,6 +471,12 @@ def rasterize_gaussians_backward(background, means3D, radii, colors, segments, s
     dL_drotations, dL_dsegments).  Gradients of absent (empty) inputs are zero tensors of the
     reference's shapes ([P,3] / [P,6] / [P,0,3] / [P,3] / [P,4] / [P,2], rasterize_points.cu:
     166-177), as read-only stride-0 views of one zero (no memory traffic)."""
+    if _HOST is not None and sh_rows is None:  # the same work in C++ (csrc/host_ext.cpp)
+        return _HOST.rasterize_gaussians_backward(background, means3D, radii, colors, segments, scales, rotations,
+                                                  float(scale_modifier), cov3D_precomp, viewmatrix, projmatrix,
+                                                  float(tan_fovx), float(tan_fovy), dL_dout_color, dL_dout_segment,
+                                                  dL_dout_depth, dL_dout_alpha, sh, int(degree), campos, geomBuffer,
+                                                  int(R), binningBuffer, imageBuffer, alpha, bool(debug))
     P = int(means3D.size(0))
     shaped = next(t for t in (dL_dout_color, dL_dout_segment, dL_dout_depth, dL_dout_alpha, alpha) if t is not None)
     H, W = int(shaped.size(-2)), int(shaped.size(-1))

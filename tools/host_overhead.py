@@ -35,6 +35,33 @@ class _Stamped:
         return r
 
 
+class _Host:
+    """The C++ host binding (gsr_host) with its two entry points stamped; its lib_ns() counter
+    gives the part of each call spent inside libgsr (launches + the num_rendered wait)."""
+
+    def __init__(self, host, log):
+        self._h, self._log = host, log
+
+    def _call(self, tag, fn, *a):
+        self._log.append((tag + "_in", time.perf_counter_ns()))
+        l0 = self._h.lib_ns()
+        r = fn(*a)
+        lib = self._h.lib_ns() - l0
+        t = time.perf_counter_ns()
+        self._log.append((tag + "_lib", lib))
+        self._log.append((tag + "_out", t))
+        return r
+
+    def rasterize_gaussians(self, *a):
+        return self._call("f", self._h.rasterize_gaussians, *a)
+
+    def rasterize_gaussians_backward(self, *a):
+        return self._call("b", self._h.rasterize_gaussians_backward, *a)
+
+    def __getattr__(self, k):
+        return getattr(self._h, k)
+
+
 class _Lib:
     def __init__(self, lib, log):
         self._lib, self._log = lib, log
@@ -64,7 +91,11 @@ def main():
     ups = [(torch.randn(c, H, W, generator=gen) * 1e-3).to(dev) for c in (3, 1, 1, 2)]
     params = [means3D, shs, opac, scales, rots, segs, means2D]
     log = []
-    _C._lib = _Lib(_C._lib, log)
+    cpp = _C._HOST is not None
+    if cpp:
+        _C._HOST = _Host(_C._HOST, log)
+    else:
+        _C._lib = _Lib(_C._lib, log)
 
     def step():
         log.append(("s", time.perf_counter_ns()))
@@ -94,18 +125,41 @@ def main():
         step()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps * 1e6
-    ph = {k: [] for k in ("py_fwd_pre", "c_fwd", "fwd_to_bwd", "c_bwd", "py_bwd_post", "total")}
+    ph = {k: [] for k in ("py_fwd_pre", "c_fwd", "fwd_to_bwd", "c_bwd", "py_bwd_post", "total",
+                          "host_excl_lib")}
     i = 0
-    while i < len(log):
-        seq = log[i:i + 6]
-        i += 6
-        if [t for t, _ in seq] != ["s", "f_in", "f_out", "b_in", "b_out", "e"]:
-            continue
-        t = [v for _, v in seq]
-        for k, a, b in (("py_fwd_pre", 0, 1), ("c_fwd", 1, 2), ("fwd_to_bwd", 2, 3), ("c_bwd", 3, 4),
-                        ("py_bwd_post", 4, 5), ("total", 0, 5)):
-            ph[k].append((t[b] - t[a]) / 1e3)
-    print(f"{cfg}: {len(ph['total'])} steps, wall {wall:.1f} us/step (GPU-synchronised loop)")
+    if cpp:
+        # C++ route: the stamps bracket the binding's calls; lib = the time inside libgsr.  The
+        # binding's own host work is counted in py_fwd_pre / fwd_to_bwd / py_bwd_post, so that the
+        # phases mean what they mean for the ctypes route (host time outside the libgsr calls).
+        names = ["s", "f_in", "f_lib", "f_out", "b_in", "b_lib", "b_out", "e"]
+        while i < len(log):
+            seq = log[i:i + 8]
+            i += 8
+            if [t for t, _ in seq] != names:
+                continue
+            t = dict(seq)
+            fh = (t["f_out"] - t["f_in"] - t["f_lib"]) / 1e3  # binding's host work around gsr_forward
+            bh = (t["b_out"] - t["b_in"] - t["b_lib"]) / 1e3
+            ph["py_fwd_pre"].append((t["f_in"] - t["s"]) / 1e3 + fh)
+            ph["c_fwd"].append(t["f_lib"] / 1e3)
+            ph["fwd_to_bwd"].append((t["b_in"] - t["f_out"]) / 1e3 + bh)
+            ph["c_bwd"].append(t["b_lib"] / 1e3)
+            ph["py_bwd_post"].append((t["e"] - t["b_out"]) / 1e3)
+            ph["total"].append((t["e"] - t["s"]) / 1e3)
+    else:
+        while i < len(log):
+            seq = log[i:i + 6]
+            i += 6
+            if [t for t, _ in seq] != ["s", "f_in", "f_out", "b_in", "b_out", "e"]:
+                continue
+            t = [v for _, v in seq]
+            for k, a, b in (("py_fwd_pre", 0, 1), ("c_fwd", 1, 2), ("fwd_to_bwd", 2, 3), ("c_bwd", 3, 4),
+                            ("py_bwd_post", 4, 5), ("total", 0, 5)):
+                ph[k].append((t[b] - t[a]) / 1e3)
+    ph["host_excl_lib"] = [a + b + c for a, b, c in zip(ph["py_fwd_pre"], ph["fwd_to_bwd"], ph["py_bwd_post"])]
+    print(f"{cfg}: {len(ph['total'])} steps, wall {wall:.1f} us/step (GPU-synchronised loop); host binding: "
+          f"{'C++ (gsr_host)' if cpp else 'ctypes'}")
     for k, v in ph.items():
         print(f"  {k:12s} median {np.median(v):8.1f} us  p90 {np.percentile(v, 90):8.1f}")
 

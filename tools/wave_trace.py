@@ -65,6 +65,32 @@ def analyse(name, tr, slots):
     print(f"   SIMDs used {len(ends)}; per-SIMD last end: min {min(ends.values()) / 1e3:.1f} "
           f"median {np.median(list(ends.values())) / 1e3:.1f} max {max(ends.values()) / 1e3:.1f} us; "
           f"per-SIMD sum of wave durations: median {np.median(work) / 1e3:.0f} max {work.max() / 1e3:.0f} us")
+    if name == "k_render_bwd":
+        # list segments (mode bits 16 front / 32 back): positions replayed = top - seg_lo
+        ck = int(os.environ.get("GSR_CKPT", "256"))
+        kind = np.where(mode & 32, 2, np.where(mode & 16, 1, 0))
+        pos = np.where(kind == 2, np.maximum(depth - ck, 0), depth)
+        for kd, lab in ((0, "whole"), (1, "front"), (2, "back")):
+            sel = kind == kd
+            if sel.any():
+                print(f"   {lab:5s}: {sel.sum()} waves, positions mean {pos[sel].mean():.0f} max {pos[sel].max()}, "
+                      f"duration mean {dur[sel].mean() / 1e3:.1f} us, start mean {s[sel].mean() / 1e3:.1f} us")
+        # the tail: waves still running when the last wave starts
+        ls = s.max()
+        tail = e > ls
+        order = np.argsort(-e[tail])[:12]
+        print(f"   {tail.sum()} waves running at the last start ({ls / 1e3:.1f} us); the 12 that end last "
+              f"(start us, end us, kind, positions, simd waves alive):")
+        for i in order:
+            j = np.nonzero(tail)[0][i]
+            same = (simd == simd[j]) & (s <= ls) & (e > ls)
+            print(f"     {s[j] / 1e3:7.1f} {e[j] / 1e3:7.1f} {('whole', 'front', 'back')[kind[j]]:5s} {pos[j]:4d} "
+                  f"{int(same.sum())}")
+        # positions still to replay at the last start, per SIMD (linear progress model)
+        frac_left = np.clip((e - ls) / np.maximum(e - s, 1), 0, 1) * tail
+        left = np.bincount(np.unique(simd, return_inverse=True)[1], weights=frac_left * pos)
+        print(f"   positions left at the last start per SIMD: median {np.median(left):.0f} p90 "
+              f"{np.percentile(left, 90):.0f} max {left.max():.0f}")
     return dict(start=s, end=e, depth=depth, n=n, xcc=xcc, mode=mode, hwid=hwid, simd=simd)
 
 
