@@ -5,7 +5,8 @@ build() compiles it in-tree into build/ext_host/ (torch.utils.cpp_extension, hos
 hipify pass; linked against libgsr.so); __graft_entry__.build() runs it.  load() returns the
 prebuilt module, or None when it has not been built -- _C.py then does the same work over
 ctypes (the same libgsr kernels; there is no CPU path either way).  GSR_HOST_EXT=0 forces the
-ctypes route (A/B of the host overhead)."""
+ctypes route (A/B of the host overhead); so does GSR_LIBRARY naming another build of libgsr (the
+module is linked against the in-tree libgsr.so, the ctypes route loads the named one)."""
 import hashlib
 import importlib.util
 import os
@@ -47,6 +48,9 @@ def build(verbose=False):
 def load():
     if os.environ.get("GSR_HOST_EXT", "1") == "0":
         return None
+    lib = os.environ.get("GSR_LIBRARY")
+    if lib and os.path.realpath(lib) != os.path.realpath(os.path.join(_HERE, "libgsr.so")):
+        return None  # a variant library (GSR_LIBRARY): the module links the in-tree libgsr.so
     path = so_path()
     try:
         with open(os.path.join(BUILD, "source.sha")) as f:

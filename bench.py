@@ -51,7 +51,7 @@ SIMD_CLOCK_HZ = 2.4e9  # MI355X peak engine clock
 # newest committed counter summary (tools/pmc.sh + tools/pmc_summary.py); its counter-derived
 # fields are reported only when it was collected on the sources being benchmarked
 PMC_SUMMARY = next((os.path.join(ROOT, "profiles", f) for f in
-                    ("round5_pmc_summary.json", "round4_pmc_summary.json", "round3_pmc_summary.json",
+                    ("round6_pmc_summary.json", "round5_pmc_summary.json", "round4_pmc_summary.json", "round3_pmc_summary.json",
                      "round2_pmc_summary.json", "round1_pmc_summary.json")
                     if os.path.exists(os.path.join(ROOT, "profiles", f))), "")
 
@@ -427,7 +427,14 @@ def main():
                                         rs.projmatrix, rs.tanfovx, rs.tanfovy, ups["color"], ups["segment"],
                                         ups["depth"], ups["alpha"], shs, deg, rs.campos, geom, R, binning, img,
                                         alpha, False)
-        return int(_C.debug_state("written", P, W, H, R, geom, binning, img).sum()) if R > 0 else 0
+        if R <= 0:
+            return 0, 0
+        wr = int(_C.debug_state("written", P, W, H, R, geom, binning, img).sum())
+        # instances whose records the render backward reads: every position below its tile's deepest
+        # contributor (front + back segments together), i.e. the sum of the per-tile max n_contrib
+        # (equal to the GSR_STATS build's count, tools/fetched_instances.py)
+        nct = _C.debug_state("n_contrib_tiles", P, W, H, R, geom, binning, img).view(-1, 256)
+        return wr, int(nct.max(dim=1).values.to(torch.int64).sum())
 
     def timed(fn, k, per_step=None, stride=1, dom_mask=0):
         """k steps between a barrier + device sync on both sides; max over ranks.  Python's
@@ -536,7 +543,7 @@ def main():
     _C._lib.gsr_timing_enable(0)
     kms, kcnt = collect()
     I, HW = int(state["I"]), W * H
-    Wrec = written_records()  # gradient records the render backward stores (gaussian_bwd's bytes)
+    Wrec, Ibwd = written_records()  # gradient records stored (gaussian_bwd's bytes); instances the backward reads
     stages = {}
     for i in range(nst):
         if scnt[i]:
@@ -577,6 +584,14 @@ def main():
                 "measured_copy_peak": measured_peak,
                 "frac_of_measured_peak": round(achieved / measured_peak, 4) if measured_peak else None,
                 "algorithmic_bytes_per_launch": algorithmic_bytes(dom, P, I, HW, deg, B, written=Wrec),
+                # SURVEY s8(d) counts every instance (52 B x num_rendered); early termination means the
+                # render backward reads only the positions below each tile's deepest contributor
+                # (Ibwd, measured here): the same kernel time against those bytes
+                "fetched_instances": Ibwd if dom == "render_bwd" else None,
+                "achieved_fetched": (round(algorithmic_bytes(dom, P, Ibwd, HW, deg, B) / (avg_live * 1e-3) / 1e9, 1)
+                                     if dom == "render_bwd" else None),
+                "frac_fetched": (round(algorithmic_bytes(dom, P, Ibwd, HW, deg, B) / (avg_live * 1e-3) / 1e9
+                                       / HBM_PEAK_GBS, 4) if dom == "render_bwd" else None),
                 "avg_launch_ms": round(avg_live, 4),
                 "launches_timed": int(cnt[dom_i]) if avg_window else int(kcnt[dom_i]),
                 "timing": (f"avg_launch_ms = mean of the hipEvent brackets libgsr records on its launch stream "
@@ -615,7 +630,7 @@ def main():
         "config": {"workload": f"{args.config}: P={P} Gaussians, SH{deg}, {W}x{H}, fwd+bwd per view; {B} view(s) per "
                                f"rank per step" + (" (per-view forward, one multi-view backward)" if B > 1 else
                                                    " through the drop-in GaussianRasterizer"), "P": P, "width": W, "height": H, "sh_degree": deg,
-                   "num_classes": 2, "num_rendered": I, "written_records": Wrec, "global_batch": world * B, "views_per_step_per_gpu": B,
+                   "num_classes": 2, "num_rendered": I, "written_records": Wrec, "bwd_fetched_instances": Ibwd, "global_batch": world * B, "views_per_step_per_gpu": B,
                    "parallelism": f"dp{world}" + ((" (views sharded; " +
                                                    EXCHANGE_DESC[step.exchange].format(lib=dinfo["collective_lib"]) +
                                                    " per step, overlapped with the next step's render)")

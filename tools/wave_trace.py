@@ -91,7 +91,8 @@ def analyse(name, tr, slots):
         left = np.bincount(np.unique(simd, return_inverse=True)[1], weights=frac_left * pos)
         print(f"   positions left at the last start per SIMD: median {np.median(left):.0f} p90 "
               f"{np.percentile(left, 90):.0f} max {left.max():.0f}")
-    return dict(start=s, end=e, depth=depth, n=n, xcc=xcc, mode=mode, hwid=hwid, simd=simd)
+    tile = (tr[:, 2] & 0xFFFFFF).astype(np.int64)
+    return dict(start=s, end=e, depth=depth, n=n, xcc=xcc, mode=mode, hwid=hwid, simd=simd, tile=tile)
 
 
 def main():
