@@ -302,6 +302,10 @@ int gsr_set_option(const char* name, long long value) {
         gsr::set_split4_bucket((int)value);
         return 0;
     }
+    if (std::string(name) == "fwd_order_cap") {  // forward tile order: lengths >= v share one bucket; 0 = off
+        gsr::set_fwd_order_cap((int)value);
+        return 0;
+    }
     if (std::string(name) == "split_bwd_depth") {  // render backward: tiles this deep on two waves; 0 = off
         gsr::set_split_buckets(gsr::split_fwd_bucket(), (int)value);
         return 0;

@@ -1025,7 +1025,7 @@ __global__ void __launch_bounds__(ORDER_THREADS) k_tile_order(uint2* __restrict_
 // not needed.
 __global__ void __launch_bounds__(256) k_tile_order_counted(const uint2* __restrict__ ranges, int T,
                                                             uint32_t* bw, uint32_t* __restrict__ order,
-                                                            int split_fwd, int split4_fwd) {
+                                                            int split_fwd, int split4_fwd, uint32_t fb_cap) {
     __shared__ uint32_t boff[FINE_BUCKETS];
     const int tid = threadIdx.x;
     if (tid < 64) {  // heavy first: exclusive offsets over buckets 131, 130, ..., 1; then bucket 0
@@ -1067,7 +1067,7 @@ __global__ void __launch_bounds__(256) k_tile_order_counted(const uint2* __restr
     }
     const int t = blockIdx.x * 256 + tid;
     const bool valid = t < T;
-    const uint32_t b = valid ? len_fbucket(ranges[t]) : 0u;
+    const uint32_t b = valid ? len_fbucket(ranges[t], fb_cap) : 0u;
     uint64_t peers = __ballot(valid);
 #pragma unroll
     for (int k = 0; k < 8; ++k) {  // buckets 0..131
@@ -1291,11 +1291,18 @@ void set_split_buckets(int fwd_bucket, int bwd_depth) {
 int split_bwd_depth() { return g_split_bwd_depth; }
 int split_fwd_bucket() { return g_split_fwd; }
 
+#ifndef GSR_FWD_ORDER_CAP
+#define GSR_FWD_ORDER_CAP 0
+#endif
+static uint32_t g_fwd_order_fb_cap = len_fbucket_n(GSR_FWD_ORDER_CAP);
+void set_fwd_order_cap(int instances) { g_fwd_order_fb_cap = instances > 0 ? len_fbucket_n((uint32_t)instances) : 0u; }
+uint32_t fwd_order_fb_cap() { return g_fwd_order_fb_cap; }
+
 void launch_tile_order_counted(const uint2* ranges, int T, uint32_t* bucket_words, uint32_t* order,
                                hipStream_t st) {
     if (T == 0) return;
     hipLaunchKernelGGL(k_tile_order_counted, dim3((unsigned)cdiv((size_t)T, 256)), dim3(256), 0, st, ranges, T,
-                       bucket_words, order, g_split_fwd, g_split4_fwd);
+                       bucket_words, order, g_split_fwd, g_split4_fwd, g_fwd_order_fb_cap);
 }
 
 void launch_tile_order(uint2* ranges, int T, uint32_t* order, hipStream_t st) {

@@ -410,7 +410,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
                                                          uint32_t* __restrict__ point_list, uint32_t cap,
                                                          const uint32_t* __restrict__ n_total,
                                                          uint2* __restrict__ ranges, uint4* zero, size_t nzero16,
-                                                         uint32_t* __restrict__ bucket_words) {
+                                                         uint32_t* __restrict__ bucket_words, uint32_t fb_cap) {
     extern __shared__ uint32_t dyn[];
     uint32_t* bits = dyn;
     uint32_t* pre = dyn + gx * RB_S;
@@ -470,7 +470,7 @@ __global__ void __launch_bounds__(RB_CH) k_tiles_scatter(int gx, int gy, int nch
             b = min(b, cap);
             const uint2 rg = b > a ? make_uint2(a, b) : make_uint2(0u, 0u);
             ranges[(size_t)y * gx + tid] = rg;
-            const uint32_t bk = len_fbucket(rg);
+            const uint32_t bk = len_fbucket(rg, fb_cap);
             if (bk) atomicAdd(&s_bc[bk], 1u);
         }
         const uint32_t cn = c + gridDim.x;
@@ -568,7 +568,7 @@ void launch_rows_binning(int P, int gx, int gy, const uint32_t* order, uint32_t*
         launch_scan_exclusive(table2, base2, n2, len2, S2, st);
         hipLaunchKernelGGL(k_tiles_scatter, dim3(grid2), dim3(RB_CH), 2 * gx * RB_S * 4, st, gx, gy, nch1, table1,
                            base1, base2, e_gid, e_x, point_list, cap32, n_total, ranges, written,
-                           written16, bucket_words);
+                           written16, bucket_words, fwd_order_fb_cap());
     } else {  // heavy-first tile order from the bucket counts (binning.hip)
         launch_tile_order_counted(ranges, gx * gy, bucket_words, tile_order, st);
     }

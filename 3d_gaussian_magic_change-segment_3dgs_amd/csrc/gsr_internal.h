@@ -53,12 +53,23 @@ __device__ __forceinline__ uint32_t len_bucket(uint2 r) {
 // Finer schedule bucket of the row-binning path: quarter octaves, 4 * bit length + the two bits
 // below the leading one (0 = empty, up to 131).  Bit length B <-> fine buckets [4B, 4B + 3].
 constexpr int FINE_BUCKETS = 132;
-__device__ __forceinline__ uint32_t len_fbucket(uint2 r) {
+__host__ __device__ inline uint32_t len_fbucket_n(uint32_t len) {
+    if (!len) return 0;
+    uint32_t bl = 0;
+    for (uint32_t v = len; v; v >>= 1) ++bl;
+    const uint32_t sub = bl >= 3 ? (len >> (bl - 3)) & 3u : (len << (3 - bl)) & 3u;
+    return 4 * bl + sub;
+}
+// fb_cap > 0: every tile at or above that fine bucket shares it (the forward's work follows the
+// depth at which its pixels terminate, not the list length, once the list is long: such tiles are
+// then issued in no particular order among themselves; gsr_set_option "fwd_order_cap")
+__device__ __forceinline__ uint32_t len_fbucket(uint2 r, uint32_t fb_cap = 0) {
     const uint32_t len = r.y - r.x;
     if (!len) return 0;
     const uint32_t bl = 32 - __clz(len);
     const uint32_t sub = bl >= 3 ? (len >> (bl - 3)) & 3u : (len << (3 - bl)) & 3u;
-    return 4 * bl + sub;
+    const uint32_t b = 4 * bl + sub;
+    return fb_cap && b > fb_cap ? fb_cap : b;
 }
 // Bucket-count words of the row binning's tile order (k_tiles_scatter counts the non-empty fine
 // buckets, k_tile_order_counted ranks the tiles): counts at [0, 132), positions at [256, 388).
@@ -353,6 +364,9 @@ size_t sort_zero_bytes(size_t n, int passes);
 void set_split_buckets(int fwd_bucket, int bwd_depth);  // negative: the built-in default
 // forward quarter tiles: tiles with n >= 2^(B-1) get four waves (0 = off; negative: default)
 void set_split4_bucket(int fwd_bucket);
+// forward tile order: list lengths at or above this many instances share one schedule bucket (0 = off)
+void set_fwd_order_cap(int instances);
+uint32_t fwd_order_fb_cap();
 int split4_fwd_bucket();
 int split_bwd_depth();
 int split_fwd_bucket();
