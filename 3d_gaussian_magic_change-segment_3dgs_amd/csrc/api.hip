@@ -302,6 +302,10 @@ int gsr_set_option(const char* name, long long value) {
         gsr::set_split4_bucket((int)value);
         return 0;
     }
+    if (std::string(name) == "fwd_xcd_pairs") {  // forward: a split tile's halves on one XCD (b, b + 8)
+        gsr::set_fwd_xcd_pairs((int)value);
+        return 0;
+    }
     if (std::string(name) == "fwd_order_cap") {  // forward tile order: lengths >= v share one bucket; 0 = off
         gsr::set_fwd_order_cap((int)value);
         return 0;

@@ -366,6 +366,8 @@ void set_split_buckets(int fwd_bucket, int bwd_depth);  // negative: the built-i
 void set_split4_bucket(int fwd_bucket);
 // forward tile order: list lengths at or above this many instances share one schedule bucket (0 = off)
 void set_fwd_order_cap(int instances);
+// forward: the two halves of a split tile on blocks b and b + 8 (one XCD) instead of b and b + 1
+void set_fwd_xcd_pairs(int on);
 uint32_t fwd_order_fb_cap();
 int split4_fwd_bucket();
 int split_bwd_depth();

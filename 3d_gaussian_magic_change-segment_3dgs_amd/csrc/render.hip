@@ -308,6 +308,10 @@ constexpr uint32_t CK_MIN_BACK = GSR_CK_MIN_BACK;  // a back segment of at least
 #define GSR_BWD_CKPT 256
 #endif
 static int g_bwd_ckpt = GSR_BWD_CKPT;
+#ifndef GSR_FWD_XCD_PAIRS
+#define GSR_FWD_XCD_PAIRS 0
+#endif
+static int g_fwd_xcd_pairs = GSR_FWD_XCD_PAIRS;  // gsr_set_option("fwd_xcd_pairs", 0 / 1)
 __device__ __forceinline__ void publish_depth(const TileSched& ts, int T, int tile, int parts, uint32_t d, int ck) {
     if (parts == 2) {
         const uint32_t old = atomicAdd(&ts.tdone[tile], (d << 1) | 1u);
@@ -621,7 +625,8 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD
                                                    const float4* __restrict__ rec, const float* __restrict__ bg,
                                                    float* __restrict__ out_color, float* __restrict__ out_depth,
                                                    float* __restrict__ out_alpha, float* __restrict__ out_segment,
-                                                   uint32_t* __restrict__ n_contrib, float* __restrict__ ckpt, int ck) {
+                                                   uint32_t* __restrict__ n_contrib, float* __restrict__ ckpt, int ck,
+                                                   int xcd_pairs) {
     __shared__ float4 srec[64][4];
     const TileSched ts = tile_sched(sched - T, T);
     if (blockIdx.x == 0 && threadIdx.x == 0) sched[SCHED_CKPT] = (uint32_t)ck;  // for the backward
@@ -633,7 +638,19 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_FWD
                     out_color, out_depth, out_alpha, out_segment, n_contrib, ckpt, ck, srec);
     } else if (b < 4 * Qs + 2 * (Hs - Qs)) {
         const uint32_t h = b - 4 * Qs;
-        fwd_tile<2>(W, H, gx, T, (int)order[Qs + (h >> 1)], 2 * (int)(h & 1), (int)b, ts, ranges, point_list, rec,
+        uint32_t ti = h >> 1, half = h & 1;
+        if (xcd_pairs) {
+            // the two halves of a tile read the same records: give them blocks b and b + 8, which
+            // the dispatcher sends to the same XCD (round robin over the 8), so the second half
+            // finds the records in that XCD's L2.  Chunks of 16 blocks = 8 tiles; the last
+            // M % 8 tiles keep the adjacent pairing.
+            const uint32_t M = Hs - Qs, full = (M / 8) * 16;
+            if (h < full) {
+                ti = 8 * (h / 16) + (h & 7);
+                half = (h >> 3) & 1;
+            }
+        }
+        fwd_tile<2>(W, H, gx, T, (int)order[Qs + ti], 2 * (int)half, (int)b, ts, ranges, point_list, rec,
                     bg, out_color, out_depth, out_alpha, out_segment, n_contrib, ckpt, ck, srec);
     } else {
         const uint32_t i = b - 2 * Qs - Hs;  // = Hs + (b - 4 Qs - 2 (Hs - Qs))
@@ -1180,6 +1197,7 @@ __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(GSR_BWD
 
 #if GSR_RENDER_PART != 2
 void set_bwd_ckpt(int pos) { g_bwd_ckpt = pos > 0 ? (pos + 63) / 64 * 64 : 0; }
+void set_fwd_xcd_pairs(int on) { g_fwd_xcd_pairs = on ? 1 : 0; }
 int bwd_ckpt() { return g_bwd_ckpt; }
 
 void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, uint32_t* sched,
@@ -1193,7 +1211,7 @@ void launch_render_forward(int W, int H, int gx, int gy, const uint32_t* order, 
     // grid for the worst case of the schedule: 2T blocks with halves only, 4T with quarters
     hipLaunchKernelGGL(k_render_fwd, dim3((split4_fwd_bucket() > 0 ? 4 : 2) * T), dim3(64), 0, st, W, H, gx, T, order,
                        sched, ranges, point_list,
-                       rec, bg, out_color, out_depth, out_alpha, out_segment, n_contrib, ckpt, ck);
+                       rec, bg, out_color, out_depth, out_alpha, out_segment, n_contrib, ckpt, ck, g_fwd_xcd_pairs);
 }
 #endif  // GSR_RENDER_PART != 2
 
