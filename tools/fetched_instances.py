@@ -5,7 +5,7 @@ contributor, so SURVEY s8(d)'s 52 B per instance x num_rendered overstates what 
 kernel can fetch (at C5 it implied 11.3 TB/s).  Counted by the GSR_STATS build (render.hip
 stat 13: the records of every batch a wave processes).
 
-Build:  make -C 3d_gaussian_magic_change-segment_3dgs_amd/csrc OUT=$PWD/build/variants/libgsr_stats.so \\
+Build:  make -C 3d_gaussian_magic_change-segment_3dgs_amd/csrc OUT=$PWD/build/diag/libgsr_stats.so \\
             HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -fno-slp-vectorize -DGSR_STATS" \
             SCHED_GAUSSIAN_BWD=      (the iterative-ilp scheduler crashes clang on the stats build)
 Run:    python tools/fetched_instances.py [config ...] > profiles/round6_fetched_instances.json   (GPU)
@@ -16,7 +16,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ.setdefault("GSR_LIBRARY", os.path.join(ROOT, "build", "variants", "libgsr_stats.so"))
+os.environ.setdefault("GSR_LIBRARY", os.path.join(ROOT, "build", "diag", "libgsr_stats.so"))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd"), os.path.join(ROOT, "tests")]
 import torch  # noqa: E402
 

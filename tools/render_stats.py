@@ -1,6 +1,6 @@
 """Wave-level loop statistics of the render kernels (instrumented build).
 
-Build:  make -C 3d_gaussian_magic_change-segment_3dgs_amd/csrc OUT=$PWD/build/variants/libgsr_stats.so \
+Build:  make -C 3d_gaussian_magic_change-segment_3dgs_amd/csrc OUT=$PWD/build/diag/libgsr_stats.so \
             HIPFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -fvisibility=hidden -DGSR_STATS"
 Run:    python tools/render_stats.py [config]      (GPU; loads the instrumented library)
 """
@@ -9,7 +9,7 @@ import os
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-os.environ.setdefault("GSR_LIBRARY", os.path.join(ROOT, "build", "variants", "libgsr_stats.so"))
+os.environ.setdefault("GSR_LIBRARY", os.path.join(ROOT, "build", "diag", "libgsr_stats.so"))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "3d_gaussian_magic_change-segment_3dgs_amd"), os.path.join(ROOT, "tests")]
 import torch  # noqa: E402
 

@@ -32,7 +32,7 @@ for cfg in c1 mt; do
 done
 grep -v amdgpu.ids $O/host_*.txt
 # instances the render kernels read (GSR_STATS build) and the per-config roofline from them
-if [ -f build/variants/libgsr_stats.so ]; then
+if [ -f build/diag/libgsr_stats.so ]; then
   timeout -k 10 300 python tools/fetched_instances.py > $O/fetched_instances.json 2> $O/fetched_instances.err || { tail -5 $O/fetched_instances.err; exit 1; }
   python tools/config_roofline.py gpurun_out/configs $O/fetched_instances.json | tee $O/config_roofline.txt
 fi

@@ -14,5 +14,5 @@ timeout -k 10 400 python3 bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench.jso
 head -c 400 $O/bench.json
 timeout -k 10 300 python tools/fetched_instances.py > $O/fetched_instances.json 2> $O/fetched_instances.err || { tail -5 $O/fetched_instances.err; exit 1; }
 cat $O/fetched_instances.err
-GSR_LIBRARY=build/variants/libgsr_wtrace.so GSR_BWD_WAVES=4 GSR_FWD_WAVES=5 timeout -k 10 300 python tools/wave_trace.py mt $O/wtrace_mt.npz > $O/wtrace_mt.txt 2>&1 || { tail -5 $O/wtrace_mt.txt; exit 1; }
+GSR_LIBRARY=build/diag/libgsr_wtrace.so GSR_BWD_WAVES=4 GSR_FWD_WAVES=5 timeout -k 10 300 python tools/wave_trace.py mt $O/wtrace_mt.npz > $O/wtrace_mt.txt 2>&1 || { tail -5 $O/wtrace_mt.txt; exit 1; }
 cat $O/wtrace_mt.txt
