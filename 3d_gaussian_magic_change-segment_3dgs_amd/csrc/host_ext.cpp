@@ -9,11 +9,14 @@
 // host-bound.  Same semantics and error messages as _C.py: float32 inputs, CPU tensors moved
 // to the device of means3D, re-allocation of misaligned inputs, the binning-capacity guess
 // passed in by the caller (speculative stage B, gsr_forward), one gradient arena with the
-// data-parallel bucket first.  No compute here: every kernel is libgsr's.
+// data-parallel bucket first.  The drop-in rasterize_gaussians() goes one step further through
+// `rasterize`: the autograd function itself is C++ (RasterizeFn below), so a training step
+// crosses into Python only at the caller's own code.  No compute here: every kernel is libgsr's.
 #include <torch/extension.h>
 #include <ATen/hip/impl/HIPGuardImplMasqueradingAsCUDA.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 
+#include <array>
 #include <atomic>
 #include <chrono>
 #include <cstdint>
@@ -95,6 +98,29 @@ at::Tensor zeros_view(const at::Device& dev, at::IntArrayRef shape) {
     at::Tensor& t = (*z)[i];
     if (!t.defined() || t.device() != dev) t = at::zeros({}, at::TensorOptions().dtype(at::kFloat).device(dev));
     return t.expand(shape);
+}
+
+long long now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+// Deferred-SH sinks (diff_gaussian_rasterization.defer_sh_gradients): their count, kept by the
+// Python context manager, and the Python function that runs a single-view backward through the
+// active sink.  A backward of the autograd route that finds a sink active (and SH coefficients)
+// hands its arguments to that function, as _RasterizeGaussians.backward would.
+std::atomic<int> g_sinks{0};
+py::object* g_sink_backward = nullptr;  // never destroyed (see zeros_view)
+
+// Host-time stamps of the autograd route (tools/host_overhead.py): per call the entry time, the
+// time inside libgsr and the exit time, steady_clock ns (CLOCK_MONOTONIC, as time.perf_counter_ns).
+std::atomic<bool> g_stamps_on{false};
+std::mutex g_stamp_mu;
+std::vector<std::array<long long, 4>> g_stamps;  // kind (0 forward, 1 backward), t_in, lib_ns, t_out
+void stamp(int kind, long long t_in, long long lib) {
+    if (!g_stamps_on.load(std::memory_order_relaxed)) return;
+    std::lock_guard<std::mutex> lk(g_stamp_mu);
+    g_stamps.push_back({kind, t_in, lib, now_ns()});
 }
 
 }  // namespace
@@ -253,11 +279,120 @@ BwdOut rasterize_gaussians_backward(
                           seg.defined() ? dsegments : zeros_view(dev, {P, GSR_NUM_CLASS}));
 }
 
+// _RasterizeGaussians (DGR/diff_gaussian_rasterization/__init__.py:46-166) as a C++ autograd
+// function: the same saved state, the same outputs (color, radii, depth, alpha, segment), radii
+// non-differentiable, unmaterialised output gradients read as zeros, and the same gradient
+// hand-back (_finish_grads: nothing for an input that needs none, a real zero tensor where an
+// input that needs one got a stride-0 placeholder).  The Python function costs ~100 us of host
+// time per view in autograd's Python hops (profiles/round6_*_host_overhead.txt); it still serves
+// debug mode (snapshot dumps) and forwards run inside defer_sh_gradients.
+using torch::autograd::AutogradContext;
+using torch::autograd::variable_list;
+
+struct RasterizeFn : public torch::autograd::Function<RasterizeFn> {
+    static variable_list forward(AutogradContext* ctx, const at::Tensor& means3D, const at::Tensor& means2D,
+                                 const at::Tensor& sh, const at::Tensor& colors, const at::Tensor& segments,
+                                 const at::Tensor& opacities, const at::Tensor& scales, const at::Tensor& rotations,
+                                 const at::Tensor& cov3D, const at::Tensor& bg, const at::Tensor& view,
+                                 const at::Tensor& proj, const at::Tensor& campos, double scale_modifier, double tanx,
+                                 double tany, int64_t H, int64_t W, int64_t degree, bool prefiltered, int64_t cap,
+                                 int64_t* num_rendered) {
+        (void)means2D;  // the screen-space gradient's carrier: it receives dmeans2D
+        const long long t_in = now_ns(), l0 = g_lib_ns.load();
+        auto [nr, color, depth, segment, alpha, radii, geom, binning, img] =
+            rasterize_gaussians(bg, means3D, colors, segments, opacities, scales, rotations, scale_modifier, cov3D,
+                                view, proj, tanx, tany, H, W, sh, degree, campos, prefiltered, false, cap);
+        *num_rendered = nr;
+        ctx->saved_data["num_rendered"] = nr;
+        ctx->saved_data["scale_modifier"] = scale_modifier;
+        ctx->saved_data["tanfovx"] = tanx;
+        ctx->saved_data["tanfovy"] = tany;
+        ctx->saved_data["sh_degree"] = degree;
+        ctx->saved_data["geom"] = geom;
+        ctx->saved_data["binning"] = binning;
+        ctx->saved_data["img"] = img;
+        ctx->save_for_backward({colors, segments, means3D, scales, rotations, cov3D, radii, sh, alpha, bg, view, proj,
+                                campos});
+        ctx->mark_non_differentiable({radii});
+        ctx->set_materialize_grads(false);
+        stamp(0, t_in, g_lib_ns.load() - l0);
+        return {color, radii, depth, alpha, segment};
+    }
+
+    static variable_list backward(AutogradContext* ctx, variable_list go) {
+        const long long t_in = now_ns(), l0 = g_lib_ns.load();
+        const auto sv = ctx->get_saved_variables();
+        const at::Tensor &colors = sv[0], &segments = sv[1], &means3D = sv[2], &scales = sv[3], &rotations = sv[4],
+                         &cov3D = sv[5], &radii = sv[6], &sh = sv[7], &alpha = sv[8], &bg = sv[9], &view = sv[10],
+                         &proj = sv[11], &campos = sv[12];
+        const int64_t nr = ctx->saved_data["num_rendered"].toInt(), degree = ctx->saved_data["sh_degree"].toInt();
+        const double sm = ctx->saved_data["scale_modifier"].toDouble(), tx = ctx->saved_data["tanfovx"].toDouble(),
+                     ty = ctx->saved_data["tanfovy"].toDouble();
+        const at::Tensor geom = ctx->saved_data["geom"].toTensor(), binning = ctx->saved_data["binning"].toTensor(),
+                         img = ctx->saved_data["img"].toTensor();
+        // output gradients in the order of the outputs: color, radii, depth, alpha, segment
+        at::Tensor g[9];
+        if (g_sinks.load() > 0 && sh.numel() > 0 && g_sink_backward) {
+            py::gil_scoped_acquire gil;
+            auto opt = [](const at::Tensor& t) { return t.defined() ? py::cast(t) : py::none(); };
+            py::tuple r = (*g_sink_backward)(bg, means3D, radii, colors, segments, scales, rotations, sm, cov3D, view,
+                                             proj, tx, ty, opt(go[0]), opt(go[4]), opt(go[2]), opt(go[3]), sh, degree,
+                                             campos, geom, nr, binning, img, alpha);
+            for (int i = 0; i < 9; ++i) g[i] = r[i].is_none() ? at::Tensor() : r[i].cast<at::Tensor>();
+        } else {
+            auto o = rasterize_gaussians_backward(bg, means3D, radii, colors, segments, scales, rotations, sm, cov3D,
+                                                  view, proj, tx, ty, go[0], go[4], go[2], go[3], sh, degree, campos,
+                                                  geom, nr, binning, img, alpha, false);
+            std::tie(g[0], g[1], g[2], g[3], g[4], g[5], g[6], g[7], g[8]) = o;
+        }
+        // (dmeans2D, dcolors, dopacity, dmeans3D, dcov3D, dsh, dscales, drot, dsegments) -> input order
+        const at::Tensor grads[9] = {g[3], g[0], g[5], g[1], g[8], g[2], g[6], g[7], g[4]};
+        variable_list out(22);  // one per forward argument; none for the settings and the scalars
+        for (int i = 0; i < 9; ++i) {
+            const at::Tensor& t = grads[i];
+            if (!t.defined() || !ctx->needs_input_grad(i)) continue;
+            bool placeholder = false;
+            if (t.numel() > 0)
+                for (int64_t st : t.strides()) placeholder |= st == 0;
+            out[i] = placeholder ? at::zeros(t.sizes(), t.options()) : t;
+        }
+        stamp(1, t_in, g_lib_ns.load() - l0);
+        return out;
+    }
+};
+
+// (color, radii, depth, alpha, segment, num_rendered); `cap`: the caller's binning-capacity guess
+// (_C.py _guess, which num_rendered then feeds)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor, at::Tensor, int64_t> rasterize(
+    const at::Tensor& means3D, const at::Tensor& means2D, const at::Tensor& sh, const at::Tensor& colors,
+    const at::Tensor& segments, const at::Tensor& opacities, const at::Tensor& scales, const at::Tensor& rotations,
+    const at::Tensor& cov3D, const at::Tensor& bg, const at::Tensor& view, const at::Tensor& proj,
+    const at::Tensor& campos, double scale_modifier, double tanx, double tany, int64_t H, int64_t W, int64_t degree,
+    bool prefiltered, int64_t cap) {
+    int64_t nr = 0;
+    auto o = RasterizeFn::apply(means3D, means2D, sh, colors, segments, opacities, scales, rotations, cov3D, bg, view,
+                                proj, campos, scale_modifier, tanx, tany, H, W, degree, prefiltered, cap, &nr);
+    return {o[0], o[1], o[2], o[3], o[4], nr};
+}
+
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, mod) {  // the single-view entry points of DGR/ext.cpp:15-19
     // the GIL is released for the whole call, as ctypes does for foreign calls: the forward
     // waits for num_rendered inside gsr_forward
     mod.def("rasterize_gaussians", &rasterize_gaussians, py::call_guard<py::gil_scoped_release>());
     mod.def("rasterize_gaussians_backward", &rasterize_gaussians_backward, py::call_guard<py::gil_scoped_release>());
+    mod.def("rasterize", &rasterize, py::call_guard<py::gil_scoped_release>());
+    mod.def("set_sinks", [](int n) { g_sinks.store(n); });
+    mod.def("set_sink_backward", [](py::object f) {
+        if (!g_sink_backward) g_sink_backward = new py::object();
+        *g_sink_backward = std::move(f);
+    });
+    mod.def("stamps", [](bool on) {  // enables / disables the stamps; returns and clears those taken
+        std::lock_guard<std::mutex> lk(g_stamp_mu);
+        g_stamps_on.store(on);
+        std::vector<std::array<long long, 4>> r;
+        r.swap(g_stamps);
+        return r;
+    });
     mod.def("version", []() { return std::string(gsr_version()); });
     mod.def("lib_ns", []() { return (long long)g_lib_ns.load(); });
 }

@@ -230,6 +230,9 @@ _BIN_GUESS = os.environ.get("GSR_BIN_GUESS", "1") != "0"
 # the single-view host work in C++ when built (_host.py; None: this module's ctypes route)
 from . import _host  # noqa: E402
 _HOST = _host.load()
+# the single-view autograd function in C++ as well (RasterizeFn; GSR_HOST_AUTOGRAD=0: the Python
+# _RasterizeGaussians over _HOST, A/B of the host overhead)
+_HOST_AUTOGRAD = _HOST if _HOST is not None and os.environ.get("GSR_HOST_AUTOGRAD", "1") != "0" else None
 _last_rendered = {}  # device -> num_rendered of the recent forwards (binning size guess)
 _GUESS_WINDOW = 16   # a trainer cycling through a batch of views sees each view's count again
 
@@ -276,6 +279,12 @@ def _record(device, num_rendered):
     recent = _last_rendered.setdefault(device, [])
     recent.append(num_rendered)
     del recent[:-_GUESS_WINDOW]
+
+
+def last_num_rendered(device):
+    """num_rendered of the latest single-view forward with P > 0 on `device` (every route records
+    it; the C++ autograd route's graph node carries no Python attributes)."""
+    return _last_rendered[device][-1]
 
 
 def rasterize_gaussians(background, means3D, colors, segments, opacity, scales, rotations, scale_modifier,

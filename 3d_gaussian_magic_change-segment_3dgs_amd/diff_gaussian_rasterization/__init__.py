@@ -60,12 +60,20 @@ class defer_sh_gradients:
     def __enter__(self):
         with _SINKS_LOCK:
             _SINKS.append(self.sink)
+            _sinks_changed()
         return self.sink
 
     def __exit__(self, *exc):
         with _SINKS_LOCK:
             _SINKS.remove(self.sink)
+            _sinks_changed()
         return False
+
+
+def _sinks_changed():
+    # the C++ autograd route (_C._HOST_AUTOGRAD) checks the count at backward time
+    if _C._HOST_AUTOGRAD is not None:
+        _C._HOST_AUTOGRAD.set_sinks(len(_SINKS))
 
 
 # the multi-view forward's side stream per device (GSR_MV_STREAMS=0: one stream)
@@ -123,6 +131,19 @@ def rasterize_gaussians(
     cov3Ds_precomp,
     raster_settings,
 ):
+    s = raster_settings
+    if _C._HOST_AUTOGRAD is not None and not s.debug and not _SINKS:
+        # the same autograd function in C++ (csrc/host_ext.cpp RasterizeFn): same outputs, saved
+        # state and gradients, without autograd's Python hops.  Debug mode (snapshot dumps) and
+        # forwards inside defer_sh_gradients take _RasterizeGaussians.
+        device = means3D.device
+        *out, num_rendered = _C._HOST_AUTOGRAD.rasterize(
+            means3D, means2D, sh, colors_precomp, segments, opacities, scales, rotations, cov3Ds_precomp, s.bg,
+            s.viewmatrix, s.projmatrix, s.campos, float(s.scale_modifier), float(s.tanfovx), float(s.tanfovy),
+            int(s.image_height), int(s.image_width), int(s.sh_degree), bool(s.prefiltered), _C._guess(device))
+        if means3D.size(0) > 0:
+            _C._record(device, num_rendered)
+        return tuple(out)
     return _RasterizeGaussians.apply(
         means3D,
         means2D,
@@ -220,12 +241,7 @@ class _RasterizeGaussians(torch.autograd.Function):
                 raster_settings.debug)
         sink = _sh_sink() if sh.numel() > 0 else None
         if sink is not None:
-            # deferred SH (view-parallel exchange): the single-view backward writes this view's
-            # exchange rows instead of dsh (include/gsr.h gsr_backward_deferred_sh)
-            rows = sink.sh_rows(1, int(means3D.size(0)), means3D.device)
-            out = _C.rasterize_gaussians_backward(*args, sh_rows=rows)
-            sink.record(rows, 1, means3D, sh, raster_settings.sh_degree, out[5], out[3],
-                        inputs=tuple(t for t in (segments, scales, rotations) if isinstance(t, torch.Tensor)))
+            out = _sink_backward(sink, args)
         elif raster_settings.debug:
             cpu_args = cpu_deep_copy_tuple(args)
             try:
@@ -252,6 +268,30 @@ class _RasterizeGaussians(torch.autograd.Function):
             None,
         )
         return _finish_grads(ctx, grads)
+
+
+def _sink_backward(sink, args):
+    """Deferred SH (view-parallel exchange): the single-view backward writes this view's exchange
+    rows instead of dsh (include/gsr.h gsr_backward_deferred_sh).  args: _C.rasterize_gaussians_backward's."""
+    means3D, segments, scales, rotations, sh, sh_degree = args[1], args[4], args[5], args[6], args[17], args[18]
+    rows = sink.sh_rows(1, int(means3D.size(0)), means3D.device)
+    out = _C.rasterize_gaussians_backward(*args, sh_rows=rows)
+    sink.record(rows, 1, means3D, sh, sh_degree, out[5], out[3],
+                inputs=tuple(t for t in (segments, scales, rotations) if isinstance(t, torch.Tensor)))
+    return out
+
+
+def _cpp_sink_backward(*args):
+    """Backward of the C++ autograd route that found a defer_sh_gradients sink active (the forward
+    ran outside the context): the sink's route, as _RasterizeGaussians.backward takes it.  args:
+    _C.rasterize_gaussians_backward's without debug."""
+    sink = _sh_sink()
+    args = args + (False,)
+    return _sink_backward(sink, args) if sink is not None else _C.rasterize_gaussians_backward(*args)
+
+
+if _C._HOST_AUTOGRAD is not None:
+    _C._HOST_AUTOGRAD.set_sink_backward(_cpp_sink_backward)
 
 
 def rasterize_gaussians_multiview(means3D, means2D_list, sh, colors_precomp, segments, opacities, scales, rotations,

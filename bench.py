@@ -398,7 +398,7 @@ def main():
                 # one view through the drop-in API (GaussianRasterizer's autograd function)
                 color, radii, depth, alpha, segment = dgr.rasterize_gaussians(means3D, means2D[0], shs, E, segs,
                                                                               opac, scales, rots, E, settings[0])
-                state["I"] = color.grad_fn.num_rendered
+                state["I"] = dgr._C.last_num_rendered(means3D.device)
                 g = torch.autograd.grad([color, depth, alpha, segment], params + means2D[:1], up_list)
             else:
                 # nv views: forward per view, one backward summing the parameter gradients

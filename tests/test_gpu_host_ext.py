@@ -14,8 +14,10 @@ pytestmark = pytest.mark.gpu
 
 
 def _both(monkeypatch, fn):
+    # the Python autograd function on both sides (tests/test_gpu_host_autograd.py: the C++ one)
     from diff_gaussian_rasterization import _C
     assert _C._HOST is not None, "gsr_host not built (__graft_entry__.build())"
+    monkeypatch.setattr(_C, "_HOST_AUTOGRAD", None)
     a = fn()
     monkeypatch.setattr(_C, "_HOST", None)
     b = fn()

@@ -1,7 +1,8 @@
 """Host-side time of one fwd+bwd step through the drop-in GaussianRasterizer (GPU).
 
-Wraps the C entry points (gsr_forward, gsr_backward) to stamp perf_counter_ns around them
-and prints, per phase, the median host microseconds over the timed steps:
+Stamps perf_counter_ns around the C entry points (gsr_forward, gsr_backward: the ctypes route),
+around the C++ binding's calls (GSR_HOST_AUTOGRAD=0), or reads the stamps the C++ autograd function
+takes itself (the default route), and prints, per phase, the median host microseconds over the timed steps:
   py_fwd_pre   step start -> gsr_forward entry (Python wrapper, argument checks, allocations)
   c_fwd        inside gsr_forward (launches + the num_rendered wait)
   fwd_to_bwd   gsr_forward exit -> gsr_backward entry (autograd, backward wrapper)
@@ -91,10 +92,13 @@ def main():
     ups = [(torch.randn(c, H, W, generator=gen) * 1e-3).to(dev) for c in (3, 1, 1, 2)]
     params = [means3D, shs, opac, scales, rots, segs, means2D]
     log = []
-    cpp = _C._HOST is not None
-    if cpp:
+    # routes: the C++ autograd function (stamps taken inside it), the Python autograd function over
+    # the C++ binding (GSR_HOST_AUTOGRAD=0) or over ctypes (GSR_HOST_EXT=0)
+    route = "autograd" if _C._HOST_AUTOGRAD is not None else "cpp" if _C._HOST is not None else "ctypes"
+    cpp = route != "ctypes"
+    if route == "cpp":
         _C._HOST = _Host(_C._HOST, log)
-    else:
+    elif route == "ctypes":
         _C._lib = _Lib(_C._lib, log)
 
     def step():
@@ -120,11 +124,22 @@ def main():
         pr.disable()
         pstats.Stats(pr).sort_stats("tottime").print_stats(35)
         log.clear()
+    if route == "autograd":
+        _C._HOST_AUTOGRAD.stamps(True)
     t0 = time.perf_counter()
     for _ in range(steps):
         step()
     torch.cuda.synchronize()
     wall = (time.perf_counter() - t0) / steps * 1e6
+    if route == "autograd":
+        # the C++ stamps (kind, t_in, lib_ns, t_out) in call order, merged into the step log
+        stamps = _C._HOST_AUTOGRAD.stamps(False)
+        fw, bw = [x for x in stamps if x[0] == 0], [x for x in stamps if x[0] == 1]
+        ss, es = [v for k, v in log if k == "s"], [v for k, v in log if k == "e"]
+        log = []
+        for s_, f, b, e in zip(ss, fw, bw, es):
+            log += [("s", s_), ("f_in", f[1]), ("f_lib", f[2]), ("f_out", f[3]), ("b_in", b[1]), ("b_lib", b[2]),
+                    ("b_out", b[3]), ("e", e)]
     ph = {k: [] for k in ("py_fwd_pre", "c_fwd", "fwd_to_bwd", "c_bwd", "py_bwd_post", "total",
                           "host_excl_lib")}
     i = 0
@@ -158,8 +173,10 @@ def main():
                             ("py_bwd_post", 4, 5), ("total", 0, 5)):
                 ph[k].append((t[b] - t[a]) / 1e3)
     ph["host_excl_lib"] = [a + b + c for a, b, c in zip(ph["py_fwd_pre"], ph["fwd_to_bwd"], ph["py_bwd_post"])]
+    names = {"autograd": "C++ autograd function (gsr_host)", "cpp": "C++ (gsr_host) under the Python autograd "
+             "function", "ctypes": "ctypes"}
     print(f"{cfg}: {len(ph['total'])} steps, wall {wall:.1f} us/step (GPU-synchronised loop); host binding: "
-          f"{'C++ (gsr_host)' if cpp else 'ctypes'}")
+          f"{names[route]}")
     for k, v in ph.items():
         print(f"  {k:12s} median {np.median(v):8.1f} us  p90 {np.percentile(v, 90):8.1f}")
 

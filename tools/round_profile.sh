@@ -25,9 +25,11 @@ python tools/pmc_summary.py $O/pmc_summary.json | grep -E "^render|^gaussian|^pr
 GSR_DIST_BACKEND=gloo timeout -k 10 400 python3 bench.py --gpus 2 --steps 20 --warmup 5 --no-train > $O/gloo2.json 2> $O/gloo2.err || { tail -20 $O/gloo2.err; exit 1; }
 bash tools/configs_bench.sh > $O/configs.txt 2>&1 || { tail -20 $O/configs.txt; exit 1; }
 cat $O/configs.txt
-# host time per view through the drop-in API (C++ host binding and the ctypes route)
+# host time per view through the drop-in API (the C++ autograd function, the Python one over the
+# C++ binding, and the ctypes route)
 for cfg in c1 mt; do
   timeout -k 10 300 python tools/host_overhead.py $cfg 300 > $O/host_${cfg}.txt 2>&1 || exit 1
+  GSR_HOST_AUTOGRAD=0 timeout -k 10 300 python tools/host_overhead.py $cfg 300 > $O/host_${cfg}_pyfn.txt 2>&1 || exit 1
   GSR_HOST_EXT=0 timeout -k 10 300 python tools/host_overhead.py $cfg 300 > $O/host_${cfg}_ctypes.txt 2>&1 || exit 1
 done
 grep -v amdgpu.ids $O/host_*.txt
