@@ -311,8 +311,13 @@ struct RasterizeFn : public torch::autograd::Function<RasterizeFn> {
         ctx->saved_data["geom"] = geom;
         ctx->saved_data["binning"] = binning;
         ctx->saved_data["img"] = img;
-        ctx->save_for_backward({colors, segments, means3D, scales, rotations, cov3D, radii, sh, alpha, bg, view, proj,
-                                campos});
+        // the settings' tensors as the Python function keeps them (ctx.raster_settings): referenced,
+        // not version-checked; the Gaussian tensors and the outputs as its save_for_backward
+        ctx->saved_data["bg"] = bg;
+        ctx->saved_data["viewmatrix"] = view;
+        ctx->saved_data["projmatrix"] = proj;
+        ctx->saved_data["campos"] = campos;
+        ctx->save_for_backward({colors, segments, means3D, scales, rotations, cov3D, radii, sh, alpha});
         ctx->mark_non_differentiable({radii});
         ctx->set_materialize_grads(false);
         stamp(0, t_in, g_lib_ns.load() - l0);
@@ -323,8 +328,9 @@ struct RasterizeFn : public torch::autograd::Function<RasterizeFn> {
         const long long t_in = now_ns(), l0 = g_lib_ns.load();
         const auto sv = ctx->get_saved_variables();
         const at::Tensor &colors = sv[0], &segments = sv[1], &means3D = sv[2], &scales = sv[3], &rotations = sv[4],
-                         &cov3D = sv[5], &radii = sv[6], &sh = sv[7], &alpha = sv[8], &bg = sv[9], &view = sv[10],
-                         &proj = sv[11], &campos = sv[12];
+                         &cov3D = sv[5], &radii = sv[6], &sh = sv[7], &alpha = sv[8];
+        const at::Tensor bg = ctx->saved_data["bg"].toTensor(), view = ctx->saved_data["viewmatrix"].toTensor(),
+                         proj = ctx->saved_data["projmatrix"].toTensor(), campos = ctx->saved_data["campos"].toTensor();
         const int64_t nr = ctx->saved_data["num_rendered"].toInt(), degree = ctx->saved_data["sh_degree"].toInt();
         const double sm = ctx->saved_data["scale_modifier"].toDouble(), tx = ctx->saved_data["tanfovx"].toDouble(),
                      ty = ctx->saved_data["tanfovy"].toDouble();

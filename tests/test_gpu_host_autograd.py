@@ -197,3 +197,24 @@ def test_cpp_autograd_errors_empty_and_debug(gpu_available, monkeypatch):
                                                       shs=d["sh"], segments=d["segments"], scales=d["scales"],
                                                       rotations=d["rotations"])
     assert "RasterizeFn" not in out[0].grad_fn.name()
+
+
+def test_cpp_autograd_settings_changed_in_place(gpu_available, monkeypatch):
+    """The settings' tensors are referenced, not version-checked, as the Python function keeps them
+    (ctx.raster_settings): a camera moved in place between the forward and the backward gives both
+    routes the same gradients and no error."""
+    scene = synthetic_scene(5000, sh_degree=3, seed=74)
+    cam = orbit_camera(1, 160, 120, 150.0)
+    ups = Hn.upstream_grads(cam.height, cam.width)
+    res = {}
+    for route in ("cpp", "py"):
+        _route(monkeypatch, route)
+        st = Hn.settings_for(cam, 3, DEV)
+        d = _inputs(scene)
+        out, m2 = _forward(d, st)
+        st.viewmatrix.mul_(1.0001)  # in place, after the forward
+        st.campos.add_(0.001)
+        out["color"].backward(ups["color"].to(DEV))
+        res[route] = _grads(d, m2)
+    monkeypatch.undo()
+    _assert_same(res["cpp"], res["py"])
