@@ -7,7 +7,7 @@ cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 R=${1:-2}
 mkdir -p gpurun_out/abk
-K="k_render_bwd1 k_render_fwd k_gaussian_backward k_preprocess k_tiles_scatter"
+K=${AB_KERNELS:-"k_render_bwd1 k_render_fwd k_gaussian_backward k_preprocess k_tiles_scatter"}
 shopt -s nullglob
 for r in $(seq 1 $R); do
   for so in "" build/variants/libgsr_*.so; do
