@@ -74,6 +74,7 @@ constexpr int RB_STAGE1 = 4 * RB_CH1;  // its row entries assembled in LDS (more
 #define GSR_RB_GRID2 768
 #endif
 constexpr int RB_CH = GSR_RB_CH;      // level 2: row entries per chunk = threads per block
+static_assert(RB_CH == 512 || RB_CH == 1024, "level-2 chunks: 16 or 32 bitmask words per bucket, at most 1024 threads");
 constexpr int RB_W = RB_CH / 32;      // bitmask words per bucket
 // LDS words per bucket row of bits / pre: one pad word so that the words of different
 // buckets fall in different banks (with a stride of 16 words, lanes touching buckets 4
@@ -88,6 +89,9 @@ constexpr int RB_GRID2 = GSR_RB_GRID2;  // blocks of the level-2 kernels (grid-s
 // (the ds_bpermute shuffles they replace were the latency chain of every level-2 chunk).
 template <int W>
 __device__ __forceinline__ uint32_t scan_incl(uint32_t x) {
+    // row_shr stays inside a 16-lane row, not inside a smaller group: W < 16 would add the previous
+    // group's lanes (wrong ranks, so wrong point_list entries)
+    static_assert(W == 16 || W == 32 || W == 64, "scan_incl: groups of 16, 32 or 64 lanes");
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x111, 0xF, 0xF, true);  // row_shr:1
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x112, 0xF, 0xF, true);  // row_shr:2
     x += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x114, 0xF, 0xF, true);  // row_shr:4
