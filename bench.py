@@ -601,7 +601,7 @@ def main():
                            f"bracketed (untimed stage pass, inflated by the brackets); rocprofv3 --kernel-trace of "
                            f"this command, the metric phase's launches picked out by tools/ktrace_phases.py (the "
                            f"trace's kernel_stats average also holds the batched and train-step launches): "
-                           f"profiles/round6_b_kernel_phases.txt"),
+                           f"profiles/round6_c_kernel_phases.txt"),
                 "avg_launch_ms_timed_region": round(avg_window, 4) if avg_window else None,
                 "avg_launch_ms_kernel_pass": round(avg_pass, 4),
                 "avg_launch_ms_stage_pass": round(sms[dom_i] / scnt[dom_i], 4) if scnt[dom_i] else None,
