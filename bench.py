@@ -492,12 +492,18 @@ def main():
         cand = {modelled: step}
         other = "allreduce" if modelled == "sh" else "sh"
         cand[other] = make_step(B, force=other)
-        trial = {}
-        for kind, fn in cand.items():
+        # two alternating rounds, the faster per exchange: one round each in a fixed order let the
+        # first candidate carry the warm-up (world 1: 0.95 vs 0.90 ms per step in the trial, 0.849
+        # vs 0.859 in steady state, profiles/round6_c_rccl_world1.txt).  Every value is the max over ranks, so every
+        # rank picks the same exchange.
+        trial = {kind: float("inf") for kind in cand}
+        for fn in cand.values():
             for _ in range(3):
                 fn()
-            drain()
-            trial[kind] = timed(fn, 8) / 8
+        drain()
+        for _ in range(2):
+            for kind, fn in cand.items():
+                trial[kind] = min(trial[kind], timed(fn, 8) / 8)
         step = cand[min(trial, key=trial.get)]
         step.exchange_trial_ms = {k: round(1e3 * v, 4) for k, v in trial.items()}
         step.exchange_modelled = modelled
