@@ -247,6 +247,24 @@ def stream_copy_peak(lib, device, nbytes=1 << 30):
     return round(best, 1)
 
 
+def exchange_trial(cand, timed, drain, rounds=2, steps=8, warm=3):
+    """The measured exchange choice: cand maps an exchange name to its step function; after `warm`
+    untimed steps of each, `rounds` alternating rounds of `steps` timed steps per exchange (timed
+    returns the max over ranks), each exchange keeping its faster round.  One round each in a fixed
+    order let the first candidate carry the warm-up (world 1: 0.95 vs 0.90 ms per step in the trial,
+    0.849 vs 0.859 in steady state, profiles/round6_c_rccl_world1.txt).  Every value is the max over
+    ranks, so every rank picks the same exchange.  Returns (chosen name, {name: seconds per step})."""
+    trial = {kind: float("inf") for kind in cand}
+    for fn in cand.values():
+        for _ in range(warm):
+            fn()
+    drain()
+    for _ in range(rounds):
+        for kind, fn in cand.items():
+            trial[kind] = min(trial[kind], timed(fn, steps) / steps)
+    return min(trial, key=trial.get), trial
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -492,19 +510,8 @@ def main():
         cand = {modelled: step}
         other = "allreduce" if modelled == "sh" else "sh"
         cand[other] = make_step(B, force=other)
-        # two alternating rounds, the faster per exchange: one round each in a fixed order let the
-        # first candidate carry the warm-up (world 1: 0.95 vs 0.90 ms per step in the trial, 0.849
-        # vs 0.859 in steady state, profiles/round6_c_rccl_world1.txt).  Every value is the max over ranks, so every
-        # rank picks the same exchange.
-        trial = {kind: float("inf") for kind in cand}
-        for fn in cand.values():
-            for _ in range(3):
-                fn()
-        drain()
-        for _ in range(2):
-            for kind, fn in cand.items():
-                trial[kind] = min(trial[kind], timed(fn, 8) / 8)
-        step = cand[min(trial, key=trial.get)]
+        chosen, trial = exchange_trial(cand, timed, drain)
+        step = cand[chosen]
         step.exchange_trial_ms = {k: round(1e3 * v, 4) for k, v in trial.items()}
         step.exchange_modelled = modelled
     nst = _C._lib.gsr_num_stages()
